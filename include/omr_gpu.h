@@ -1,0 +1,190 @@
+/*
+ * omr_gpu.h — C ABI of the MI355X-native InstantOMR detector (libomr_gpu.so).
+ *
+ * This is the drop-in boundary for the detect path of xiangxiecrypto/tfhe-omr. Each entry
+ * point names the reference interface it replaces (file:line under omr_core/src/). A Rust
+ * caller binds these with `extern "C"` declarations; Python tests and
+ * bench.py bind them with ctypes. Plain C: no exceptions cross the boundary, every call
+ * returns an omr_status and omr_last_error() returns the thread-local message of the last
+ * failure.
+ *
+ * Data conventions (identical to the parity oracle, oracle/omr_oracle.h):
+ *  - RLWE (a, b), b = a*s + e + m over Z_q[X]/(X^N+1). LWE (a, b), b = <a,s> + e + m.
+ *  - NTT domain: index j holds p(psi^(2*brv(j)+1)), psi = g^((q-1)/2N), g = 7 (q1), 22 (q2).
+ *  - Keys cross the boundary in the COEFFICIENT domain, canonical residues in [0, q):
+ *      bsk1      u32 [512][8][2][1024]   GGSW_{s1}(s0_i), rows 0..3 a-gadget, 4..7 b-gadget
+ *      ksk       u32 [1024][27][671]     LWE_{s_int}(s1_i * 2^j): a[670], b
+ *      bsk2      u64 [670][12][2][2048]  GGSW_{s2}(s_int_i), rows 0..5 a-gadget, 6..11 b-gadget
+ *      trace_key u64 [11][25][2][2048]   step k (g = 2048/2^k + 1), digit j:
+ *                                        (alpha, alpha*s2 + e - sigma_g(s2) * 4^j)
+ *    GGSW(m) row k = (alpha_k + m*g_k, alpha_k*s + e_k); row d+k = (alpha', alpha'*s + e' + m*g_k),
+ *    gadget g_k = 2^(drop + k*logB): BR1 (logB 5, d 4, drop 7), BR2 (logB 7, d 6, drop 8).
+ *  - A clue (CmLweCiphertext<u16>) is mask a[512] and bodies b[7], values mod 2048.
+ *  - A pertinency ciphertext (NttRlweCiphertext<SecondLevelField>) is u64 [2][2048] (a then b),
+ *    NTT domain, canonical residues mod q2.
+ */
+#ifndef OMR_GPU_H
+#define OMR_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Parameter set: omr_core/src/parameters/mod.rs:39-105 */
+#define OMR_N0 512
+#define OMR_Q0 2048
+#define OMR_CLUE_COUNT 7
+#define OMR_Q1 134215681u
+#define OMR_N1 1024
+#define OMR_KS_DIGITS 27
+#define OMR_NI 670
+#define OMR_QI 4096
+#define OMR_Q2 1125899906826241ull
+#define OMR_N2 2048
+#define OMR_TRACE_STEPS 11
+#define OMR_TRACE_DIGITS 25
+#define OMR_P 257
+#define OMR_PAYLOAD_LEN 612
+
+typedef enum {
+  OMR_OK = 0,
+  OMR_ERR_INVALID_ARGUMENT = 1,
+  OMR_ERR_DEVICE = 2,
+  OMR_ERR_OUT_OF_MEMORY = 3,
+  OMR_ERR_NOT_INVERTIBLE = 4 /* OmrError::InvertibleMatrix, error.rs:5-8 */
+} omr_status;
+
+/* Message of the last failing call on this thread ("" if none). */
+const char *omr_last_error(void);
+/* Library / build identification, e.g. "omr_gpu 0.1 gfx950". */
+const char *omr_version(void);
+
+/* ---------------------------------------------------------------------------------------
+ * Key generation (CPU) — KeyGen::generate_secret_key (key_gen/mod.rs:21-27),
+ * SecretKeyPack::new (key_gen/secret.rs:46-95), generate_sender (:110), generate_detection_key
+ * (:118-178). Deterministic from a 64-bit seed (counter-based ChaCha12 streams per key row),
+ * so every rank of a multi-GPU job derives identical keys.
+ * ------------------------------------------------------------------------------------- */
+typedef struct omr_secret_key_pack omr_secret_key_pack;
+
+omr_status omr_keygen_secret(uint64_t seed, omr_secret_key_pack **out);
+void omr_secret_destroy(omr_secret_key_pack *sk);
+/* Secret material for client-side checks: s0 (512 bits), s1 (1024 ternary), s_int (670 bits),
+ * s2 (2048 ternary). Any pointer may be NULL. */
+omr_status omr_secret_export(const omr_secret_key_pack *sk, uint8_t *s0, int8_t *s1,
+                             uint8_t *s_int, int8_t *s2);
+/* DetectionKey in the coefficient-domain layout above. nthreads <= 0: all host cores. */
+omr_status omr_keygen_detection_key(const omr_secret_key_pack *sk, uint64_t seed, uint32_t *bsk1,
+                                    uint32_t *ksk, uint64_t *bsk2, uint64_t *trace_key,
+                                    int nthreads);
+/* Sender::gen_clues (sender.rs:27-32, key_gen/clue.rs:27-34): `count` clues (7 encryptions of 0
+ * under the pack's RLWE-mode public key) for global message indices [first, first+count).
+ * clue_a u16 [count][512], clue_b u16 [count][7]. */
+omr_status omr_gen_clues(const omr_secret_key_pack *sk, uint64_t seed, uint64_t first,
+                         size_t count, uint16_t *clue_a, uint16_t *clue_b, int nthreads);
+
+/* ---------------------------------------------------------------------------------------
+ * Retrieval layout — RetrievalParams::new(257, 2048, all, pertinent, 130, 25, 2)
+ * (parameters/retrieval_params.rs:50-106; arguments as in key_gen/secret.rs:189-209).
+ * ------------------------------------------------------------------------------------- */
+typedef struct {
+  uint32_t index_slots_per_bucket, slots_per_bucket, slots_per_segment, segment_per_cipher,
+      max_encode_indices_cipher_count, combination_count, cmb_count_per_cipher, cmb_cipher_count;
+} omr_retrieval_params;
+omr_status omr_get_retrieval_params(size_t all_payloads_count, size_t pertinent_count,
+                                    omr_retrieval_params *out);
+/* Payload weights: StdRng::from_seed(seed) + Uniform<u16>(0,257), drawn in the reference's
+ * order (detector.rs:376-387): out[j*all + i] for combination j < combination_count, the rest
+ * zero; out has cmb_cipher_count*cmb_count_per_cipher*all entries. */
+omr_status omr_payload_weights(const uint8_t seed[32], size_t all_payloads_count,
+                               uint32_t combination_count, uint32_t cmb_cipher_count,
+                               uint32_t cmb_count_per_cipher, uint16_t *out);
+
+/* ---------------------------------------------------------------------------------------
+ * Detector — one context per GPU; calls on one context are serialised; contexts are
+ * independent. Detector::new (detector.rs:85-110) uploads the keys and converts them to the
+ * device layout; the LUTs (:457-503) are built inside.
+ * ------------------------------------------------------------------------------------- */
+typedef struct omr_ctx omr_ctx;
+
+typedef struct {
+  const uint32_t *bsk1;
+  const uint32_t *ksk;
+  const uint64_t *bsk2;
+  const uint64_t *trace_key;
+} omr_detection_key_view;
+
+omr_status omr_ctx_create(const omr_detection_key_view *key, int device, omr_ctx **out);
+void omr_ctx_destroy(omr_ctx *ctx);
+/* Messages per internal batch (memory/latency knob); 0 = default. */
+omr_status omr_ctx_set_batch(omr_ctx *ctx, size_t batch);
+
+/* Detector::detect (detector.rs:135-166), batched like `par_iter().map(detect)` in
+ * examples/omr.rs:219-223. Host buffers: clue_a u16 [D][512], clue_b u16 [D][7],
+ * out u64 [D][2][2048] (NTT domain). */
+omr_status omr_detect_batch(omr_ctx *ctx, const uint16_t *clue_a, const uint16_t *clue_b,
+                            size_t D, uint64_t *out);
+/* Same on device buffers, enqueued on `hip_stream` (NULL = the context's stream);
+ * returns once enqueued. */
+omr_status omr_detect_batch_device(omr_ctx *ctx, const uint16_t *d_clue_a,
+                                   const uint16_t *d_clue_b, size_t D, uint64_t *d_out,
+                                   void *hip_stream);
+
+/* Detector::detect_with_time_info (detector.rs:169-221): device time of the last detect call
+ * per stage, milliseconds (recorded only when enabled; enabling adds events per stage). */
+typedef struct {
+  float total_ms, first_level_ms, key_switch_ms, second_level_ms; /* second_level includes trace */
+  size_t messages;
+} omr_detect_timing;
+omr_status omr_ctx_enable_timing(omr_ctx *ctx, int enable);
+omr_status omr_last_timing(omr_ctx *ctx, omr_detect_timing *t);
+
+/* Detector::encode_pertinent_indices (detector.rs:223-339) for index ciphertext `ct` over the
+ * messages with global indices [global_offset, global_offset+D) of an all_payloads_count board.
+ * Buckets come from a seeded counter-based stream (the reference uses thread_rng, :262) so
+ * that shards agree. out u64 [2][2048] (NTT domain), a partial digest summed mod q2 across
+ * shards. */
+omr_status omr_encode_indices(omr_ctx *ctx, const uint64_t *pv, size_t D, size_t global_offset,
+                              size_t all_payloads_count, uint64_t seed, uint32_t ct,
+                              uint64_t *out);
+omr_status omr_encode_indices_device(omr_ctx *ctx, const uint64_t *d_pv, size_t D,
+                                     size_t global_offset, size_t all_payloads_count,
+                                     uint64_t seed, uint32_t first_ct, uint32_t n_ct,
+                                     uint64_t *d_out /* [n_ct][2][2048] */, void *hip_stream);
+/* Detector::encode_pertinent_payloads (detector.rs:341-453). weights: omr_payload_weights()
+ * output for the whole board; payloads u16 [D][612]; out u64 [n_ct][2][2048]. */
+omr_status omr_encode_payloads(omr_ctx *ctx, const uint64_t *pv, const uint16_t *payloads,
+                               size_t D, size_t global_offset, size_t all_payloads_count,
+                               const uint16_t *weights, uint32_t n_ct, uint32_t cmb_per_ct,
+                               uint64_t *out);
+omr_status omr_encode_payloads_device(omr_ctx *ctx, const uint64_t *d_pv,
+                                      const uint16_t *d_payloads, size_t D, size_t global_offset,
+                                      size_t all_payloads_count, const uint16_t *d_weights,
+                                      uint32_t n_ct, uint32_t cmb_per_ct, uint64_t *d_out,
+                                      void *hip_stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Stage entry points (for parity tests and per-stage benchmarks, benches/two_level_bs.rs).
+ * Host buffers.
+ * ------------------------------------------------------------------------------------- */
+/* First level (detector.rs:533-597) for D messages: out u32 [D][671] (a[670], b mod 4096). */
+omr_status omr_first_level(omr_ctx *ctx, const uint16_t *clue_a, const uint16_t *clue_b,
+                           size_t D, uint32_t *lwe_int);
+/* One level-1 blind rotation per LWE (a u16 [n][512], b u16 [n]): out u64 [n][2][1024]. */
+omr_status omr_blind_rotate_level1(omr_ctx *ctx, const uint16_t *lwe_a, const uint16_t *lwe_b,
+                                   size_t n, uint64_t *out);
+/* Second level + trace (detector.rs:599-639) on LWE(670, 4096) inputs: out u64 [n][2][2048]. */
+omr_status omr_second_level(omr_ctx *ctx, const uint32_t *lwe_int, size_t n, uint64_t *out);
+/* Level-2 blind rotation only (no trace): out u64 [n][2][2048] coefficient domain. */
+omr_status omr_blind_rotate_level2(omr_ctx *ctx, const uint32_t *lwe_int, size_t n,
+                                   uint64_t *out);
+/* Forward / inverse NTT of n polynomials (level 1: N=1024 mod q1, level 2: N=2048 mod q2). */
+omr_status omr_ntt(int level, int inverse, uint64_t *polys, size_t n, int device);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

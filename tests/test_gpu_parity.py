@@ -1,0 +1,156 @@
+"""GPU parity: every HIP stage through the C ABI against the oracle / golden vectors, bit-exact."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+import product_lib as PL
+import retriever as R
+from product_lib import omr_amd as A
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(PL.ROOT, "tests", "golden")
+
+
+@pytest.fixture(scope="module")
+def prim():
+    with open(os.path.join(GOLDEN, "primitives.json")) as f:
+        return json.load(f)
+
+
+@pytest.mark.parametrize("level", [1, 2])
+def test_gpu_ntt_matches_definition(prim, level):
+    vecs = prim["ntt"][str(level)]
+    inp = np.array([v["in"] for v in vecs], dtype=np.uint64)
+    out = A.ntt(level, inp)
+    assert out.tolist() == [v["out"] for v in vecs]
+    back = A.ntt(level, out, inverse=True)
+    assert np.array_equal(back, inp)
+    # random batch vs oracle
+    q = A.Q1 if level == 1 else A.Q2
+    n = 1024 if level == 1 else 2048
+    rnd = np.random.default_rng(level).integers(0, q, (64, n), dtype=np.uint64)
+    g = A.ntt(level, rnd)
+    for k in range(0, 64, 9):
+        assert np.array_equal(g[k], O.ntt(level, rnd[k]))
+    assert np.array_equal(A.ntt(level, g, inverse=True), rnd)
+
+
+@pytest.fixture(scope="module")
+def structured():
+    import structured_keys
+    keys, expect = structured_keys.load()
+    dk = A.DetectionKey(keys["bsk1"], keys["ksk"], keys["bsk2"], keys["tk"])
+    det = A.Detector(dk)
+    yield det, expect
+    det.close()
+
+
+def test_structured_stages(structured):
+    det, e = structured
+    la = np.zeros(512, dtype=np.uint16)
+    lb = np.zeros(1, dtype=np.uint16)
+    O.lib().oref_extract_clue(e["clue_a"], e["clue_b"], 0, la, lb)
+    assert np.array_equal(det.blind_rotate_level1(la, lb)[0], e["br1_clue0"])
+    assert np.array_equal(det.first_level(e["clue_a"], e["clue_b"])[0], e["lwe_int"])
+    assert np.array_equal(det.blind_rotate_level2(e["lwe_int"])[0], e["br2"])
+    assert np.array_equal(det.second_level(e["lwe_int"])[0], e["detect"])
+    assert np.array_equal(det.detect(e["clue_a"], e["clue_b"]), e["detect"])
+
+
+@pytest.fixture(scope="module")
+def real():
+    a, b, dk = PL.keys()
+    det = A.Detector(dk)
+    orc = O.OracleDetector(dk.bsk1, dk.ksk, dk.bsk2, dk.trace_key)
+    yield a, det, orc
+    det.close()
+    orc.close()
+
+
+def test_real_keys_detect_bit_exact_and_kat(real):
+    a, det, orc = real
+    s2 = a.export()["s2"]
+    mask = np.array([1, 0, 1, 0, 0, 1, 0, 1], dtype=bool)
+    ca, cb = PL.mixed_clues(mask, seed=31)
+    gpu = det.detect_batch(ca, cb)
+    ref = orc.detect_batch(ca, cb)
+    assert np.array_equal(gpu, ref)
+    for m in range(len(mask)):
+        dec = R.decrypt_decode(s2, gpu[m])
+        if mask[m]:
+            assert dec[0] == 1 and not dec[1:].any()
+        else:
+            assert not dec.any()
+
+
+def test_real_keys_stage_parity(real):
+    _, det, orc = real
+    ca, cb = PL.mixed_clues([True, False, False], seed=7)
+    fl = det.first_level(ca, cb)
+    for m in range(3):
+        assert np.array_equal(fl[m], orc.first_level(ca[m], cb[m]))
+    br = det.blind_rotate_level2(fl[:1])
+    assert np.array_equal(br[0], orc.br2(fl[0]))
+    assert np.array_equal(det.second_level(fl[:1])[0], orc.trace(br[0]))
+
+
+def test_encode_golden(structured):
+    det, _ = structured
+    z = np.load(os.path.join(GOLDEN, "encode.npz"))
+    pv = z["pv"]
+    all_count = int(z["all_count"])
+    rp = A.RetrievalParams(all_count, 0)
+    for k, ct in enumerate(z["idx_cts"]):
+        got = det.encode_pertinent_indices(rp, pv, int(z["seed"]), int(ct), global_offset=int(z["offset"]))
+        assert np.array_equal(got, z["idx"][k])
+    n_ct, per_ct = int(z["n_ct"]), int(z["per_ct"])
+    w, _ = O.payload_weights(z["wseed"].tobytes(), n_ct * per_ct * all_count)
+    rp.cmb_cipher_count, rp.cmb_count_per_cipher = n_ct, per_ct
+    got = det.encode_pertinent_payloads(pv, z["payloads"], w, rp, global_offset=int(z["offset"]))
+    assert np.array_equal(got, z["pay"])
+
+
+def test_batch_1024_kat_and_sampled_parity(real):
+    """Config 2 size (1024 clues): every output decrypts correctly; sampled messages bit-exact."""
+    a, det, orc = real
+    s2 = a.export()["s2"]
+    D = 1024
+    rng = np.random.default_rng(3)
+    mask = np.zeros(D, dtype=bool)
+    mask[rng.choice(D, 50, replace=False)] = True
+    ca, cb = PL.mixed_clues(mask, seed=2024)
+    det.set_batch(512)  # exercise the chunk loop
+    out = det.detect_batch(ca, cb)
+    det.set_batch(0)
+    for m in range(D):
+        dec = R.decrypt_decode(s2, out[m])
+        assert (dec[0] == 1) == mask[m]
+        assert not dec[1:].any()
+    for m in (0, 511, 512, int(np.nonzero(mask)[0][0])):
+        assert np.array_equal(out[m], orc.detect(ca[m], cb[m]))
+
+
+def test_end_to_end_gpu_retrieval(real):
+    a, det, orc = real
+    s2 = a.export()["s2"]
+    D = 300
+    rng = np.random.default_rng(8)
+    mask = np.zeros(D, dtype=bool)
+    mask[rng.choice(D, 12, replace=False)] = True
+    ca, cb = PL.mixed_clues(mask, seed=555)
+    pv = det.detect_batch(ca, cb)
+    payloads = rng.integers(0, 256, (D, 612)).astype(np.uint16)
+    rp = A.RetrievalParams(D, int(mask.sum()))
+    idx = [det.encode_pertinent_indices(rp, pv, 9, ct) for ct in range(rp.max_encode_indices_cipher_count)]
+    assert np.array_equal(idx[0], O.encode_indices(pv, 0, D, 9, 0))
+    found = R.decode_indices(s2, idx, vars(rp), int(mask.sum()))
+    assert found == set(np.nonzero(mask)[0].tolist())
+    w = A.payload_weights(bytes(range(1, 33)), rp)
+    pay = det.encode_pertinent_payloads(pv, payloads, w, rp)
+    assert np.array_equal(pay[:2], O.encode_payloads(pv, payloads, 0, D, w, 2, 2))
+    solved = R.decode_payloads(s2, pay, w, D, sorted(found), rp.combination_count)
+    for i, p in zip(sorted(found), solved):
+        assert p == payloads[i].tolist()

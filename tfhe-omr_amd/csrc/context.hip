@@ -1,0 +1,580 @@
+// Detector context: device-resident keys and tables, batch orchestration and the C ABI of
+// include/omr_gpu.h for the detect / encode path.
+//
+// Detector::new (detector.rs:85-110) -> omr_ctx_create: uploads the coefficient-domain keys,
+// converts them on the GPU to centred FP64 NTT-domain rows (N^-1 folded into the external-
+// product keys) and builds the LUTs (:457-503). Detector::detect (:135-166) for a batch of
+// messages -> four launches per chunk: br1_kernel (7 blind rotations per message), sum7_kernel,
+// ks_kernel, br2_trace_kernel.
+#include <algorithm>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "detect_kernels.hpp"
+#include "encode_kernels.hpp"
+
+using namespace omr;
+
+#define HIP_TRY(expr)                                                                     \
+  do {                                                                                    \
+    hipError_t _e = (expr);                                                               \
+    if (_e != hipSuccess)                                                                 \
+      return set_error(OMR_ERR_DEVICE, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+  } while (0)
+
+namespace {
+
+typedef unsigned __int128 u128;
+
+uint64_t h_mulmod(uint64_t a, uint64_t b, uint64_t q) { return (uint64_t)((u128)a * b % q); }
+uint64_t h_powmod(uint64_t b, uint64_t e, uint64_t q) {
+  uint64_t r = 1;
+  b %= q;
+  while (e) {
+    if (e & 1) r = h_mulmod(r, b, q);
+    b = h_mulmod(b, b, q);
+    e >>= 1;
+  }
+  return r;
+}
+double centred(uint64_t v, uint64_t q) { return v > (q - 1) / 2 ? (double)v - (double)q : (double)v; }
+uint32_t h_brv(uint32_t x, int bits) { return __builtin_bitreverse32(x) >> (32 - bits); }
+
+// psi^brv(k), psi^-brv(k) as centred doubles (the convention of include/omr_gpu.h).
+void twiddles(uint64_t q, int N, uint64_t g, std::vector<double> &tw, std::vector<double> &itw) {
+  const int L = __builtin_ctz(N);
+  const uint64_t psi = h_powmod(g, (q - 1) / (2 * (uint64_t)N), q);
+  const uint64_t ipsi = h_powmod(psi, q - 2, q);
+  tw.resize(N);
+  itw.resize(N);
+  for (int k = 0; k < N; ++k) {
+    const uint32_t e = h_brv((uint32_t)k, L);
+    tw[k] = centred(h_powmod(psi, e, q), q);
+    itw[k] = centred(h_powmod(ipsi, e, q), q);
+  }
+}
+
+// LookUpTable::negacyclic_lut (lut.rs:12-27): chunk c of N >> log_t coefficients holds
+// v[(c+1)/2] (itertools::interleave(v, v[1..])).
+std::vector<double> negacyclic_lut(const std::vector<uint64_t> &v, int N, int log_t, uint64_t q) {
+  std::vector<double> lut(N, 0.0);
+  const int hd = N >> log_t;
+  for (int c = 0; c < N / hd; ++c) {
+    const size_t idx = (size_t)(c + 1) / 2;
+    const uint64_t val = idx < v.size() ? v[idx] : 0;
+    for (int j = 0; j < hd; ++j) lut[c * hd + j] = centred(val, q);
+  }
+  return lut;
+}
+
+}  // namespace
+
+struct omr_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  double *bsk1 = nullptr, *bsk2 = nullptr, *tk = nullptr;
+  uint32_t *ksk = nullptr;
+  double *tables = nullptr;  // tw1 itw1 tw2 itw2 lut1 lut2
+  uint16_t *trace_tabs = nullptr;
+  DeviceTables tb{};
+  size_t batch = 16384, batch_cap = 0;
+  uint32_t *ext = nullptr, *lwe1t = nullptr, *lwe_int = nullptr;
+  // host-API staging
+  uint16_t *s_clue_a = nullptr, *s_clue_b = nullptr;
+  uint64_t *s_out = nullptr;
+  size_t staged = 0;
+  // encode workspace
+  uint64_t *partial = nullptr;
+  size_t partial_cap = 0;
+  // timing
+  bool timing = false;
+  std::vector<hipEvent_t> events;  // 5 per chunk
+  size_t timed_messages = 0;
+  std::mutex mu;
+};
+
+namespace {
+
+omr_status ensure_batch(omr_ctx *c, size_t B) {
+  if (B <= c->batch_cap) return OMR_OK;
+  hipFree(c->ext);
+  hipFree(c->lwe1t);
+  hipFree(c->lwe_int);
+  c->ext = nullptr;
+  c->lwe1t = nullptr;
+  c->lwe_int = nullptr;
+  HIP_TRY(hipMalloc(&c->ext, B * CLUES * (N1 + 1) * sizeof(uint32_t)));
+  HIP_TRY(hipMalloc(&c->lwe1t, B * (N1 + 1) * sizeof(uint32_t)));
+  HIP_TRY(hipMalloc(&c->lwe_int, B * (NI + 1) * sizeof(uint32_t)));
+  c->batch_cap = B;
+  return OMR_OK;
+}
+
+omr_status ensure_partial(omr_ctx *c, size_t elems) {
+  if (elems <= c->partial_cap) return OMR_OK;
+  hipFree(c->partial);
+  c->partial = nullptr;
+  HIP_TRY(hipMalloc(&c->partial, elems * sizeof(uint64_t)));
+  c->partial_cap = elems;
+  return OMR_OK;
+}
+
+template <int LEVEL, typename IN>
+omr_status convert_keys(const IN *host, size_t npoly, double *dev, double scale, const double *tw,
+                        hipStream_t st) {
+  constexpr int N = Mod<LEVEL>::N;
+  constexpr int T = LEVEL == 1 ? BR1_T : BR2_T;
+  const size_t chunk = 4096;  // polynomials per upload
+  IN *tmp = nullptr;
+  HIP_TRY(hipMalloc(&tmp, chunk * N * sizeof(IN)));
+  for (size_t p0 = 0; p0 < npoly; p0 += chunk) {
+    const size_t n = std::min(chunk, npoly - p0);
+    HIP_TRY(hipMemcpyAsync(tmp, host + p0 * N, n * N * sizeof(IN), hipMemcpyHostToDevice, st));
+    key_to_ntt_kernel<LEVEL, IN><<<n, T, 0, st>>>(tmp, dev + p0 * N, n, scale, tw);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(st));
+  }
+  hipFree(tmp);
+  return OMR_OK;
+}
+
+}  // namespace
+
+// Scale the even (alpha) rows of the trace key by N^-1 in place.
+__global__ void scale_even_rows_kernel(double *rows, size_t npoly, double s) {
+  using M = Mod<2>;
+  const size_t poly = (size_t)blockIdx.x * 2;
+  if (poly >= npoly) return;
+  double *p = rows + poly * N2;
+  for (int j = threadIdx.x; j < N2; j += blockDim.x) p[j] = canon<M>(mm<M>(p[j], s));
+}
+
+extern "C" omr_status omr_ctx_create(const omr_detection_key_view *key, int device, omr_ctx **out) {
+  if (!key || !out || !key->bsk1 || !key->ksk || !key->bsk2 || !key->trace_key)
+    return set_error(OMR_ERR_INVALID_ARGUMENT, "omr_ctx_create: NULL key component");
+  int ndev = 0;
+  HIP_TRY(hipGetDeviceCount(&ndev));
+  if (device < 0 || device >= ndev)
+    return set_error(OMR_ERR_INVALID_ARGUMENT, "omr_ctx_create: no such device");
+  HIP_TRY(hipSetDevice(device));
+  auto *c = new omr_ctx();
+  c->device = device;
+  auto fail = [&](omr_status st) {
+    omr_ctx_destroy(c);
+    return st;
+  };
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
+    return fail(set_error(OMR_ERR_DEVICE, "hipStreamCreate failed"));
+  // tables
+  std::vector<double> tw1, itw1, tw2, itw2;
+  twiddles(Q1, N1, 7, tw1, itw1);
+  twiddles(Q2, N2, 22, tw2, itw2);
+  const uint64_t one1 = ((Q1 >> 4) + 1) >> 1;  // detector.rs:457-476
+  auto lut1 = negacyclic_lut({one1, 0, 0, 0, Q1 - one1}, N1, 3, Q1);
+  std::vector<uint64_t> v2(TI, 0);
+  v2[2 * CLUES] = (2 * Q2 + P) / (2 * P);  // round_half_up(q2/257), detector.rs:479-503
+  auto lut2 = negacyclic_lut(v2, N2, 5, Q2);
+  std::vector<double> tabs;
+  for (auto *v : {&tw1, &itw1, &tw2, &itw2, &lut1, &lut2}) tabs.insert(tabs.end(), v->begin(), v->end());
+  std::vector<uint16_t> ttab(2 * TRACE_STEPS * N2);
+  for (int k = 0; k < TRACE_STEPS; ++k) {
+    const uint32_t g = (uint32_t)(N2 >> k) + 1;
+    for (int i = 0; i < N2; ++i) {  // sigma_g: coefficient i -> position i*g mod 2N
+      const uint32_t e = (uint32_t)(((uint64_t)i * g) % (2 * N2));
+      if (e < (uint32_t)N2) ttab[k * N2 + e] = (uint16_t)i;
+      else ttab[k * N2 + (e - N2)] = (uint16_t)(i + N2);
+    }
+    for (int t = 0; t < N2; ++t) {  // NTT domain: value at t comes from t' with eps(t') = g*eps(t)
+      const uint32_t eps = 2 * h_brv((uint32_t)t, 11) + 1;
+      const uint32_t e2 = (uint32_t)(((uint64_t)eps * g) % (2 * N2));
+      ttab[(TRACE_STEPS + k) * N2 + t] = (uint16_t)h_brv((e2 - 1) / 2, 11);
+    }
+  }
+  if (hipMalloc(&c->tables, tabs.size() * sizeof(double)) != hipSuccess ||
+      hipMalloc(&c->trace_tabs, ttab.size() * sizeof(uint16_t)) != hipSuccess)
+    return fail(set_error(OMR_ERR_OUT_OF_MEMORY, "omr_ctx_create: tables"));
+  hipMemcpy(c->tables, tabs.data(), tabs.size() * sizeof(double), hipMemcpyHostToDevice);
+  hipMemcpy(c->trace_tabs, ttab.data(), ttab.size() * sizeof(uint16_t), hipMemcpyHostToDevice);
+  c->tb.tw1 = c->tables;
+  c->tb.itw1 = c->tables + N1;
+  c->tb.tw2 = c->tables + 2 * N1;
+  c->tb.itw2 = c->tables + 2 * N1 + N2;
+  c->tb.lut1 = c->tables + 2 * N1 + 2 * N2;
+  c->tb.lut2 = c->tables + 3 * N1 + 2 * N2;
+  c->tb.trace_src = c->trace_tabs;
+  c->tb.trace_perm = c->trace_tabs + TRACE_STEPS * N2;
+  // keys
+  if (hipMalloc(&c->bsk1, BSK1_ELEMS * sizeof(double)) != hipSuccess ||
+      hipMalloc(&c->bsk2, BSK2_ELEMS * sizeof(double)) != hipSuccess ||
+      hipMalloc(&c->tk, TK_ELEMS * sizeof(double)) != hipSuccess ||
+      hipMalloc(&c->ksk, (KSK_ELEMS + 64) * sizeof(uint32_t)) != hipSuccess)
+    return fail(set_error(OMR_ERR_OUT_OF_MEMORY, "omr_ctx_create: key buffers"));
+  const double ninv1 = centred(h_powmod(N1, Q1 - 2, Q1), Q1);
+  const double ninv2 = centred(h_powmod(N2, Q2 - 2, Q2), Q2);
+  omr_status st;
+  if ((st = convert_keys<1, uint32_t>(key->bsk1, BSK1_ELEMS / N1, c->bsk1, ninv1, c->tb.tw1,
+                                      c->stream)) != OMR_OK)
+    return fail(st);
+  if ((st = convert_keys<2, uint64_t>(key->bsk2, BSK2_ELEMS / N2, c->bsk2, ninv2, c->tb.tw2,
+                                      c->stream)) != OMR_OK)
+    return fail(st);
+  if ((st = convert_keys<2, uint64_t>(key->trace_key, TK_ELEMS / N2, c->tk, 1.0, c->tb.tw2,
+                                      c->stream)) != OMR_OK)
+    return fail(st);
+  scale_even_rows_kernel<<<(TK_ELEMS / N2 + 1) / 2, 256, 0, c->stream>>>(c->tk, TK_ELEMS / N2, ninv2);
+  if (hipMemcpyAsync(c->ksk, key->ksk, KSK_ELEMS * sizeof(uint32_t), hipMemcpyHostToDevice,
+                     c->stream) != hipSuccess ||
+      hipMemsetAsync(c->ksk + KSK_ELEMS, 0, 64 * sizeof(uint32_t), c->stream) != hipSuccess ||
+      hipStreamSynchronize(c->stream) != hipSuccess)
+    return fail(set_error(OMR_ERR_DEVICE, "omr_ctx_create: key upload"));
+  if ((st = ensure_batch(c, c->batch)) != OMR_OK) return fail(st);
+  *out = c;
+  return OMR_OK;
+}
+
+extern "C" void omr_ctx_destroy(omr_ctx *c) {
+  if (!c) return;
+  hipSetDevice(c->device);
+  if (c->stream) hipStreamSynchronize(c->stream);
+  for (void *p : {(void *)c->bsk1, (void *)c->bsk2, (void *)c->tk, (void *)c->ksk,
+                  (void *)c->tables, (void *)c->trace_tabs, (void *)c->ext, (void *)c->lwe1t,
+                  (void *)c->lwe_int, (void *)c->s_clue_a, (void *)c->s_clue_b, (void *)c->s_out,
+                  (void *)c->partial})
+    if (p) hipFree(p);
+  for (auto e : c->events) hipEventDestroy(e);
+  if (c->stream) hipStreamDestroy(c->stream);
+  delete c;
+}
+
+extern "C" omr_status omr_ctx_set_batch(omr_ctx *c, size_t batch) {
+  if (!c) return set_error(OMR_ERR_INVALID_ARGUMENT, "omr_ctx_set_batch: NULL ctx");
+  std::lock_guard<std::mutex> lk(c->mu);
+  c->batch = batch ? batch : 16384;
+  hipSetDevice(c->device);
+  return ensure_batch(c, c->batch);
+}
+
+extern "C" omr_status omr_ctx_enable_timing(omr_ctx *c, int enable) {
+  if (!c) return set_error(OMR_ERR_INVALID_ARGUMENT, "NULL ctx");
+  c->timing = enable != 0;
+  return OMR_OK;
+}
+
+namespace {
+
+omr_status detect_device(omr_ctx *c, const uint16_t *ca, const uint16_t *cb, size_t D,
+                         uint64_t *out, hipStream_t st) {
+  omr_status s;
+  if ((s = ensure_batch(c, std::min(D, c->batch))) != OMR_OK) return s;
+  const size_t nchunks = (D + c->batch - 1) / c->batch;
+  if (c->timing) {
+    while (c->events.size() < nchunks * 5) {
+      hipEvent_t e;
+      HIP_TRY(hipEventCreate(&e));
+      c->events.push_back(e);
+    }
+    c->timed_messages = D;
+  }
+  for (size_t ch = 0; ch < nchunks; ++ch) {
+    const size_t off = ch * c->batch;
+    const int B = (int)std::min(c->batch, D - off);
+    hipEvent_t *ev = c->timing ? &c->events[ch * 5] : nullptr;
+    if (ev) HIP_TRY(hipEventRecord(ev[0], st));
+    br1_kernel<<<(unsigned)(B * CLUES), BR1_T, 0, st>>>(ca + off * N0, cb + off * CLUES, nullptr,
+                                                          nullptr, c->bsk1, c->tb, c->ext, nullptr, 0);
+    HIP_TRY(hipGetLastError());
+    if (ev) HIP_TRY(hipEventRecord(ev[1], st));
+    const size_t n7 = (size_t)B * (N1 + 1);
+    sum7_kernel<<<(unsigned)((n7 + 255) / 256), 256, 0, st>>>(c->ext, c->lwe1t, B);
+    ks_kernel<KS_CT><<<dim3((B + 63) / 64, (NI + 1 + KS_CT - 1) / KS_CT), 64, 0, st>>>(c->lwe1t, c->ksk, c->lwe_int, B);
+    HIP_TRY(hipGetLastError());
+    if (ev) HIP_TRY(hipEventRecord(ev[2], st));
+    br2_trace_kernel<<<(unsigned)B, BR2_T, 0, st>>>(c->lwe_int, c->bsk2, c->tk, c->tb,
+                                                    out + off * 2 * N2, 0);
+    HIP_TRY(hipGetLastError());
+    if (ev) HIP_TRY(hipEventRecord(ev[3], st));
+  }
+  return OMR_OK;
+}
+
+omr_status stage_buffers(omr_ctx *c, size_t B) {
+  if (B <= c->staged) return OMR_OK;
+  hipFree(c->s_clue_a);
+  hipFree(c->s_clue_b);
+  hipFree(c->s_out);
+  c->s_clue_a = nullptr;
+  c->s_clue_b = nullptr;
+  c->s_out = nullptr;
+  HIP_TRY(hipMalloc(&c->s_clue_a, B * N0 * sizeof(uint16_t)));
+  HIP_TRY(hipMalloc(&c->s_clue_b, B * CLUES * sizeof(uint16_t)));
+  HIP_TRY(hipMalloc(&c->s_out, B * 2 * N2 * sizeof(uint64_t)));
+  c->staged = B;
+  return OMR_OK;
+}
+
+}  // namespace
+
+extern "C" omr_status omr_detect_batch_device(omr_ctx *c, const uint16_t *ca, const uint16_t *cb,
+                                              size_t D, uint64_t *out, void *stream) {
+  if (!c || (D && (!ca || !cb || !out)))
+    return set_error(OMR_ERR_INVALID_ARGUMENT, "omr_detect_batch_device: NULL argument");
+  if (D == 0) return OMR_OK;
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  return detect_device(c, ca, cb, D, out, stream ? (hipStream_t)stream : c->stream);
+}
+
+extern "C" omr_status omr_detect_batch(omr_ctx *c, const uint16_t *ca, const uint16_t *cb, size_t D,
+                                       uint64_t *out) {
+  if (!c || (D && (!ca || !cb || !out)))
+    return set_error(OMR_ERR_INVALID_ARGUMENT, "omr_detect_batch: NULL argument");
+  if (D == 0) return OMR_OK;
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  omr_status s;
+  const size_t B = std::min(D, c->batch);
+  if ((s = stage_buffers(c, B)) != OMR_OK) return s;
+  for (size_t off = 0; off < D; off += B) {
+    const size_t n = std::min(B, D - off);
+    HIP_TRY(hipMemcpyAsync(c->s_clue_a, ca + off * N0, n * N0 * sizeof(uint16_t), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->s_clue_b, cb + off * CLUES, n * CLUES * sizeof(uint16_t), hipMemcpyHostToDevice, c->stream));
+    if ((s = detect_device(c, c->s_clue_a, c->s_clue_b, n, c->s_out, c->stream)) != OMR_OK) return s;
+    HIP_TRY(hipMemcpyAsync(out + off * 2 * N2, c->s_out, n * 2 * N2 * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+  }
+  return OMR_OK;
+}
+
+extern "C" omr_status omr_last_timing(omr_ctx *c, omr_detect_timing *t) {
+  if (!c || !t) return set_error(OMR_ERR_INVALID_ARGUMENT, "omr_last_timing: NULL argument");
+  memset(t, 0, sizeof(*t));
+  if (!c->timing || c->timed_messages == 0) return OMR_OK;
+  const size_t nchunks = (c->timed_messages + c->batch - 1) / c->batch;
+  for (size_t ch = 0; ch < nchunks; ++ch) {
+    hipEvent_t *ev = &c->events[ch * 5];
+    HIP_TRY(hipEventSynchronize(ev[3]));
+    float a = 0, b = 0, d = 0;
+    HIP_TRY(hipEventElapsedTime(&a, ev[0], ev[1]));
+    HIP_TRY(hipEventElapsedTime(&b, ev[1], ev[2]));
+    HIP_TRY(hipEventElapsedTime(&d, ev[2], ev[3]));
+    t->first_level_ms += a;
+    t->key_switch_ms += b;
+    t->second_level_ms += d;
+  }
+  t->total_ms = t->first_level_ms + t->key_switch_ms + t->second_level_ms;
+  t->messages = c->timed_messages;
+  return OMR_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// Encode (detector.rs:223-453)
+// ------------------------------------------------------------------------------------------
+extern "C" omr_status omr_encode_indices_device(omr_ctx *c, const uint64_t *pv, size_t D,
+                                                size_t offset, size_t all, uint64_t seed,
+                                                uint32_t first_ct, uint32_t n_ct, uint64_t *out,
+                                                void *stream) {
+  if (!c || !out || (D && !pv) || n_ct == 0 || offset + D > all)
+    return set_error(OMR_ERR_INVALID_ARGUMENT, "omr_encode_indices_device: bad argument");
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+  omr_retrieval_params rp;
+  omr_status s;
+  if ((s = omr_get_retrieval_params(all, 0, &rp)) != OMR_OK) return s;
+  if (D == 0) {
+    HIP_TRY(hipMemsetAsync(out, 0, (size_t)n_ct * 2 * N2 * sizeof(uint64_t), st));
+    return OMR_OK;
+  }
+  const int per_wg = D >= 16384 ? 128 : 32;
+  const int chunks = (int)((D + per_wg - 1) / per_wg);
+  if ((s = ensure_partial(c, (size_t)n_ct * chunks * 2 * N2)) != OMR_OK) return s;
+  EncodeLayout ly{(int)rp.index_slots_per_bucket, (int)rp.slots_per_bucket,
+                  (int)rp.slots_per_segment, (int)rp.segment_per_cipher};
+  encode_indices_kernel<<<dim3(chunks, n_ct), ENC_T, 0, st>>>(pv, (int)D, offset, ly, seed, first_ct,
+                                                              per_wg, c->tb.tw2, c->partial);
+  HIP_TRY(hipGetLastError());
+  const size_t tot = (size_t)n_ct * 2 * N2;
+  reduce_partials_kernel<<<(unsigned)((tot + 255) / 256), 256, 0, st>>>(c->partial, chunks, (int)n_ct, out);
+  HIP_TRY(hipGetLastError());
+  return OMR_OK;
+}
+
+extern "C" omr_status omr_encode_payloads_device(omr_ctx *c, const uint64_t *pv,
+                                                 const uint16_t *payloads, size_t D, size_t offset,
+                                                 size_t all, const uint16_t *weights, uint32_t n_ct,
+                                                 uint32_t per_ct, uint64_t *out, void *stream) {
+  if (!c || !out || (D && (!pv || !payloads || !weights)) || n_ct == 0 || per_ct == 0 ||
+      per_ct * PAYLOAD_LEN > (uint32_t)N2 || offset + D > all)
+    return set_error(OMR_ERR_INVALID_ARGUMENT, "omr_encode_payloads_device: bad argument");
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+  if (D == 0) {
+    HIP_TRY(hipMemsetAsync(out, 0, (size_t)n_ct * 2 * N2 * sizeof(uint64_t), st));
+    return OMR_OK;
+  }
+  const int per_wg = D >= 16384 ? 128 : 32;
+  const int chunks = (int)((D + per_wg - 1) / per_wg);
+  omr_status s;
+  if ((s = ensure_partial(c, (size_t)n_ct * chunks * 2 * N2)) != OMR_OK) return s;
+  encode_payloads_kernel<<<dim3(chunks, n_ct), ENC_T, 0, st>>>(pv, payloads, (int)D, offset, all,
+                                                               weights, (int)per_ct, per_wg,
+                                                               c->tb.tw2, c->partial);
+  HIP_TRY(hipGetLastError());
+  const size_t tot = (size_t)n_ct * 2 * N2;
+  reduce_partials_kernel<<<(unsigned)((tot + 255) / 256), 256, 0, st>>>(c->partial, chunks, (int)n_ct, out);
+  HIP_TRY(hipGetLastError());
+  return OMR_OK;
+}
+
+namespace {
+template <typename T>
+struct DevBuf {
+  T *p = nullptr;
+  ~DevBuf() {
+    if (p) hipFree(p);
+  }
+  hipError_t alloc(size_t n) { return hipMalloc(&p, n * sizeof(T)); }
+};
+}  // namespace
+
+extern "C" omr_status omr_encode_indices(omr_ctx *c, const uint64_t *pv, size_t D, size_t offset,
+                                         size_t all, uint64_t seed, uint32_t ct, uint64_t *out) {
+  if (!c || !out || (D && !pv)) return set_error(OMR_ERR_INVALID_ARGUMENT, "omr_encode_indices");
+  hipSetDevice(c->device);
+  DevBuf<uint64_t> dpv, dout;
+  HIP_TRY(dpv.alloc(std::max<size_t>(D, 1) * 2 * N2));
+  HIP_TRY(dout.alloc(2 * N2));
+  HIP_TRY(hipMemcpy(dpv.p, pv, D * 2 * N2 * sizeof(uint64_t), hipMemcpyHostToDevice));
+  omr_status s = omr_encode_indices_device(c, dpv.p, D, offset, all, seed, ct, 1, dout.p, nullptr);
+  if (s != OMR_OK) return s;
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  HIP_TRY(hipMemcpy(out, dout.p, 2 * N2 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  return OMR_OK;
+}
+
+extern "C" omr_status omr_encode_payloads(omr_ctx *c, const uint64_t *pv, const uint16_t *payloads,
+                                          size_t D, size_t offset, size_t all,
+                                          const uint16_t *weights, uint32_t n_ct, uint32_t per_ct,
+                                          uint64_t *out) {
+  if (!c || !out || (D && (!pv || !payloads || !weights)))
+    return set_error(OMR_ERR_INVALID_ARGUMENT, "omr_encode_payloads");
+  hipSetDevice(c->device);
+  const size_t wn = (size_t)n_ct * per_ct * all;
+  DevBuf<uint64_t> dpv, dout;
+  DevBuf<uint16_t> dpay, dw;
+  HIP_TRY(dpv.alloc(std::max<size_t>(D, 1) * 2 * N2));
+  HIP_TRY(dpay.alloc(std::max<size_t>(D, 1) * PAYLOAD_LEN));
+  HIP_TRY(dw.alloc(std::max<size_t>(wn, 1)));
+  HIP_TRY(dout.alloc((size_t)n_ct * 2 * N2));
+  HIP_TRY(hipMemcpy(dpv.p, pv, D * 2 * N2 * sizeof(uint64_t), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(dpay.p, payloads, D * PAYLOAD_LEN * sizeof(uint16_t), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(dw.p, weights, wn * sizeof(uint16_t), hipMemcpyHostToDevice));
+  omr_status s = omr_encode_payloads_device(c, dpv.p, dpay.p, D, offset, all, dw.p, n_ct, per_ct,
+                                            dout.p, nullptr);
+  if (s != OMR_OK) return s;
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  HIP_TRY(hipMemcpy(out, dout.p, (size_t)n_ct * 2 * N2 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  return OMR_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// Stage entry points (parity tests, per-stage benchmarks)
+// ------------------------------------------------------------------------------------------
+extern "C" omr_status omr_first_level(omr_ctx *c, const uint16_t *ca, const uint16_t *cb, size_t D,
+                                      uint32_t *lwe_int) {
+  if (!c || !ca || !cb || !lwe_int || D == 0 || D > c->batch)
+    return set_error(OMR_ERR_INVALID_ARGUMENT, "omr_first_level: bad argument (D <= batch)");
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  omr_status s;
+  if ((s = stage_buffers(c, D)) != OMR_OK || (s = ensure_batch(c, D)) != OMR_OK) return s;
+  hipStream_t st = c->stream;
+  HIP_TRY(hipMemcpyAsync(c->s_clue_a, ca, D * N0 * sizeof(uint16_t), hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemcpyAsync(c->s_clue_b, cb, D * CLUES * sizeof(uint16_t), hipMemcpyHostToDevice, st));
+  const int B = (int)D;
+  br1_kernel<<<(unsigned)(B * CLUES), BR1_T, 0, st>>>(c->s_clue_a, c->s_clue_b, nullptr, nullptr,
+                                                        c->bsk1, c->tb, c->ext, nullptr, 0);
+  const size_t n7 = (size_t)B * (N1 + 1);
+  sum7_kernel<<<(unsigned)((n7 + 255) / 256), 256, 0, st>>>(c->ext, c->lwe1t, B);
+  ks_kernel<KS_CT><<<dim3((B + 63) / 64, (NI + 1 + KS_CT - 1) / KS_CT), 64, 0, st>>>(c->lwe1t, c->ksk, c->lwe_int, B);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(lwe_int, c->lwe_int, D * (NI + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  return OMR_OK;
+}
+
+extern "C" omr_status omr_blind_rotate_level1(omr_ctx *c, const uint16_t *la, const uint16_t *lb,
+                                              size_t n, uint64_t *out) {
+  if (!c || !la || !lb || !out || n == 0)
+    return set_error(OMR_ERR_INVALID_ARGUMENT, "omr_blind_rotate_level1: bad argument");
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  DevBuf<uint16_t> da, db;
+  DevBuf<uint64_t> dout;
+  HIP_TRY(da.alloc(n * N0));
+  HIP_TRY(db.alloc(n));
+  HIP_TRY(dout.alloc(n * 2 * N1));
+  HIP_TRY(hipMemcpy(da.p, la, n * N0 * sizeof(uint16_t), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(db.p, lb, n * sizeof(uint16_t), hipMemcpyHostToDevice));
+  br1_kernel<<<(unsigned)n, BR1_T, 0, c->stream>>>(nullptr, nullptr, da.p, db.p, c->bsk1, c->tb,
+                                                   nullptr, dout.p, 1);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  HIP_TRY(hipMemcpy(out, dout.p, n * 2 * N1 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  return OMR_OK;
+}
+
+static omr_status second_level_impl(omr_ctx *c, const uint32_t *lwe, size_t n, uint64_t *out,
+                                    int mode) {
+  if (!c || !lwe || !out || n == 0)
+    return set_error(OMR_ERR_INVALID_ARGUMENT, "omr_second_level: bad argument");
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  DevBuf<uint32_t> dl;
+  DevBuf<uint64_t> dout;
+  HIP_TRY(dl.alloc(n * (NI + 1)));
+  HIP_TRY(dout.alloc(n * 2 * N2));
+  HIP_TRY(hipMemcpy(dl.p, lwe, n * (NI + 1) * sizeof(uint32_t), hipMemcpyHostToDevice));
+  br2_trace_kernel<<<(unsigned)n, BR2_T, 0, c->stream>>>(dl.p, c->bsk2, c->tk, c->tb, dout.p, mode);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  HIP_TRY(hipMemcpy(out, dout.p, n * 2 * N2 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  return OMR_OK;
+}
+
+extern "C" omr_status omr_second_level(omr_ctx *c, const uint32_t *lwe, size_t n, uint64_t *out) {
+  return second_level_impl(c, lwe, n, out, 0);
+}
+extern "C" omr_status omr_blind_rotate_level2(omr_ctx *c, const uint32_t *lwe, size_t n,
+                                              uint64_t *out) {
+  return second_level_impl(c, lwe, n, out, 1);
+}
+
+extern "C" omr_status omr_ntt(int level, int inverse, uint64_t *polys, size_t n, int device) {
+  if ((level != 1 && level != 2) || !polys || n == 0)
+    return set_error(OMR_ERR_INVALID_ARGUMENT, "omr_ntt: bad argument");
+  HIP_TRY(hipSetDevice(device));
+  const uint64_t q = level == 1 ? Q1 : Q2;
+  const int N = level == 1 ? N1 : N2;
+  std::vector<double> tw, itw;
+  twiddles(q, N, level == 1 ? 7 : 22, tw, itw);
+  DevBuf<double> dt;
+  DevBuf<uint64_t> dp;
+  HIP_TRY(dt.alloc(2 * N));
+  HIP_TRY(dp.alloc(n * N));
+  HIP_TRY(hipMemcpy(dt.p, tw.data(), N * sizeof(double), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(dt.p + N, itw.data(), N * sizeof(double), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(dp.p, polys, n * N * sizeof(uint64_t), hipMemcpyHostToDevice));
+  const double ninv = centred(h_powmod(N, q - 2, q), q);
+  if (level == 1)
+    ntt_u64_kernel<1><<<(unsigned)n, BR1_T>>>(dp.p, n, inverse, ninv, dt.p, dt.p + N);
+  else
+    ntt_u64_kernel<2><<<(unsigned)n, BR2_T>>>(dp.p, n, inverse, ninv, dt.p, dt.p + N);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(polys, dp.p, n * N * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  return OMR_OK;
+}

@@ -1,0 +1,73 @@
+// Kernels of the detect / encode path (gfx950). Each kernel cites the reference function it
+// replaces; the launch code is in context.hip.
+#pragma once
+
+#include "device_ntt.hpp"
+
+namespace omr {
+
+// Workgroup geometry per level (T threads x E residues per thread = N).
+constexpr int BR1_T = 128, BR1_E = 8;    // N1 = 1024
+constexpr int BR2_T = 128, BR2_E = 16;   // N2 = 2048
+constexpr int KS_MSGS = 64, KS_COLS = 64, KS_THREADS = 256;
+constexpr int ENC_T = 128, ENC_E = 16;
+
+struct DeviceTables {
+  const double *tw1, *itw1, *tw2, *itw2;  // psi^brv(k), psi^-brv(k) (centred)
+  const double *lut1, *lut2;              // LUTs, coefficient domain (centred)
+  const uint16_t *trace_perm;             // [11][2048] NTT-domain permutation of sigma_g
+  const uint16_t *trace_src;              // [11][2048] coefficient source index of sigma_g (+N: negate)
+};
+
+// ---- key conversion: coefficient-domain canonical residues -> NTT-domain centred doubles ----
+template <int LEVEL, typename IN>
+__global__ void key_to_ntt_kernel(const IN *in, double *out, size_t npoly, double scale,
+                                  const double *tw) {
+  using M = Mod<LEVEL>;
+  constexpr int T = LEVEL == 1 ? BR1_T : BR2_T, E = LEVEL == 1 ? BR1_E : BR2_E;
+  using NTT = WgNtt<M, T, E>;
+  __shared__ double lds[NTT::LDS_DOUBLES];
+  const size_t poly = blockIdx.x;
+  const int tid = threadIdx.x;
+  if (poly >= npoly) return;
+  const IN *src = in + poly * M::N;
+  double x[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) x[e] = from_u64<M>((uint64_t)src[tid + e * T]);
+  NTT::fwd(x, lds, tw, tid);
+  double *dst = out + poly * M::N + tid * E;
+#pragma unroll
+  for (int e = 0; e < E; ++e) dst[e] = scale == 1.0 ? canon<M>(x[e]) : canon<M>(mm<M>(canon<M>(x[e]), scale));
+}
+
+// ---- plain NTT of canonical u64 polynomials (tests / omr_ntt) ----
+template <int LEVEL>
+__global__ void ntt_u64_kernel(uint64_t *polys, size_t npoly, int inverse, double ninv,
+                               const double *tw, const double *itw) {
+  using M = Mod<LEVEL>;
+  constexpr int T = LEVEL == 1 ? BR1_T : BR2_T, E = LEVEL == 1 ? BR1_E : BR2_E;
+  using NTT = WgNtt<M, T, E>;
+  __shared__ double lds[NTT::LDS_DOUBLES];
+  const size_t poly = blockIdx.x;
+  const int tid = threadIdx.x;
+  if (poly >= npoly) return;
+  uint64_t *p = polys + poly * M::N;
+  double x[E];
+  if (!inverse) {
+#pragma unroll
+    for (int e = 0; e < E; ++e) x[e] = from_u64<M>(p[tid + e * T]);
+    NTT::fwd(x, lds, tw, tid);
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < E; ++e) p[tid * E + e] = to_u64<M>(canon<M>(x[e]));
+  } else {
+#pragma unroll
+    for (int e = 0; e < E; ++e) x[e] = from_u64<M>(p[tid * E + e]);
+    NTT::inv(x, lds, itw, tid);
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < E; ++e) p[tid + e * T] = to_u64<M>(canon<M>(mm<M>(canon<M>(x[e]), ninv)));
+  }
+}
+
+}  // namespace omr

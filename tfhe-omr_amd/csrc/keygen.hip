@@ -1,0 +1,475 @@
+// Host-side key generation, clue generation and digest-layout helpers (CPU).
+//
+// Mirrors omr_core's KeyGen / SecretKeyPack / Sender (key_gen/mod.rs:16-27,
+// key_gen/secret.rs:46-209, key_gen/clue.rs:27-34, sender.rs:27-32) and the seeded weight
+// stream of Detector::encode_pertinent_payloads (detector.rs:376-387). Every random draw comes
+// from a ChaCha12 stream keyed by (seed, domain) whose stream id is the key row (or the global
+// message index for clues), so results do not depend on thread count or sharding.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "common.hpp"
+
+namespace omr {
+
+static thread_local std::string g_last_error;
+
+omr_status set_error(omr_status st, const std::string &msg) {
+  g_last_error = msg;
+  return st;
+}
+
+namespace {
+
+typedef unsigned __int128 u128;
+
+// ------------------------------------------------------------------------------------------
+// Random streams
+// ------------------------------------------------------------------------------------------
+enum Domain : uint32_t {
+  DOM_S0 = 1, DOM_S1 = 2, DOM_SINT = 3, DOM_S2 = 4, DOM_PK_A = 5, DOM_PK_E = 6,
+  DOM_BSK1 = 10, DOM_KSK = 11, DOM_BSK2 = 12, DOM_TK = 13, DOM_CLUE = 20,
+};
+
+class Stream {
+ public:
+  Stream(uint64_t seed, uint32_t domain, uint64_t stream) : stream_(stream) {
+    key_[0] = (uint32_t)seed;
+    key_[1] = (uint32_t)(seed >> 32);
+    key_[2] = 0x6b657967u;  // "keyg"
+    key_[3] = domain;
+    for (int i = 4; i < 8; ++i) key_[i] = 0;
+  }
+  uint32_t next32() {
+    if (pos_ == 16) {
+      chacha_block(12, key_, ctr_++, stream_, buf_);
+      pos_ = 0;
+    }
+    return buf_[pos_++];
+  }
+  uint64_t next64() {
+    uint64_t lo = next32();
+    return lo | ((uint64_t)next32() << 32);
+  }
+  uint64_t uniform(uint64_t q) {  // rejection sampling on the bit length of q
+    int bits = 64 - __builtin_clzll(q - 1);
+    uint64_t mask = bits == 64 ? ~0ull : ((1ull << bits) - 1);
+    for (;;) {
+      uint64_t v = next64() & mask;
+      if (v < q) return v;
+    }
+  }
+  int ternary() {
+    for (;;) {
+      uint32_t v = next32();
+      if (v < 0xFFFFFFFFu - (0xFFFFFFFFu % 3)) return (int)(v % 3) - 1;  // {-1, 0, 1}
+    }
+  }
+  int bit() { return (int)(next32() & 1u); }
+
+ private:
+  uint32_t key_[8];
+  uint64_t stream_;
+  uint64_t ctr_ = 0;
+  uint32_t buf_[16];
+  int pos_ = 16;
+};
+
+// Rounded Gaussian by cumulative distribution table over |x| (deterministic, integer search).
+class Gaussian {
+ public:
+  explicit Gaussian(double sigma) {
+    int K = std::max(16, (int)std::ceil(sigma * 13.0) + 2);
+    std::vector<long double> w(K + 1);
+    long double Z = 0;
+    for (int k = 0; k <= K; ++k) {
+      w[k] = (k == 0 ? 1.0L : 2.0L) * std::exp(-(long double)k * k / (2.0L * sigma * sigma));
+      Z += w[k];
+    }
+    long double acc = 0;
+    table_.resize(K + 1);
+    for (int k = 0; k <= K; ++k) {
+      acc += w[k] / Z;
+      long double t = acc * 9223372036854775808.0L;  // 2^63
+      table_[k] = t >= 9223372036854775807.0L ? ~0ull >> 1 : (uint64_t)t;
+    }
+    table_[K] = ~0ull >> 1;
+  }
+  int64_t sample(Stream &s) const {
+    uint64_t u = s.next64() >> 1;
+    size_t k = std::upper_bound(table_.begin(), table_.end(), u) - table_.begin();
+    if (k >= table_.size()) k = table_.size() - 1;
+    if (k == 0) return 0;
+    return (s.next32() & 1u) ? -(int64_t)k : (int64_t)k;
+  }
+
+ private:
+  std::vector<uint64_t> table_;
+};
+
+// ------------------------------------------------------------------------------------------
+// Host negacyclic NTT (same convention as the device path and oracle/omr_oracle.h).
+// ------------------------------------------------------------------------------------------
+uint64_t mulmod(uint64_t a, uint64_t b, uint64_t q) { return (uint64_t)((u128)a * b % q); }
+uint64_t powmod(uint64_t b, uint64_t e, uint64_t q) {
+  uint64_t r = 1;
+  b %= q;
+  while (e) {
+    if (e & 1) r = mulmod(r, b, q);
+    b = mulmod(b, b, q);
+    e >>= 1;
+  }
+  return r;
+}
+uint32_t bitrev(uint32_t x, int bits) { return __builtin_bitreverse32(x) >> (32 - bits); }
+
+struct HostNtt {
+  uint64_t q;
+  int N, L;
+  std::vector<uint64_t> w, ws, iw, iws;
+  uint64_t ninv, ninvs;
+  HostNtt(uint64_t q_, int N_, uint64_t g) : q(q_), N(N_), L(__builtin_ctz(N_)) {
+    uint64_t psi = powmod(g, (q - 1) / (2 * (uint64_t)N), q), ipsi = powmod(psi, q - 2, q);
+    w.resize(N); ws.resize(N); iw.resize(N); iws.resize(N);
+    for (int k = 0; k < N; ++k) {
+      uint32_t e = bitrev((uint32_t)k, L);
+      w[k] = powmod(psi, e, q);
+      iw[k] = powmod(ipsi, e, q);
+      ws[k] = pre(w[k]);
+      iws[k] = pre(iw[k]);
+    }
+    ninv = powmod((uint64_t)N, q - 2, q);
+    ninvs = pre(ninv);
+  }
+  uint64_t pre(uint64_t v) const { return (uint64_t)(((u128)v << 64) / q); }
+  uint64_t mul(uint64_t a, uint64_t v, uint64_t vs) const {
+    uint64_t qe = (uint64_t)(((u128)a * vs) >> 64);
+    uint64_t r = a * v - qe * q;
+    return r >= q ? r - q : r;
+  }
+  void fwd(uint64_t *a) const {
+    for (int m = 1, h = N / 2; m < N; m <<= 1, h >>= 1)
+      for (int i = 0; i < m; ++i)
+        for (int j = 2 * i * h; j < 2 * i * h + h; ++j) {
+          uint64_t U = a[j], V = mul(a[j + h], w[m + i], ws[m + i]);
+          uint64_t s = U + V;
+          a[j] = s >= q ? s - q : s;
+          a[j + h] = U >= V ? U - V : U + q - V;
+        }
+  }
+  void inv(uint64_t *a) const {
+    for (int m = N / 2, h = 1; m >= 1; m >>= 1, h <<= 1)
+      for (int i = 0; i < m; ++i)
+        for (int j = 2 * i * h; j < 2 * i * h + h; ++j) {
+          uint64_t U = a[j], V = a[j + h];
+          uint64_t s = U + V;
+          a[j] = s >= q ? s - q : s;
+          a[j + h] = mul(U >= V ? U - V : U + q - V, iw[m + i], iws[m + i]);
+        }
+    for (int j = 0; j < N; ++j) a[j] = mul(a[j], ninv, ninvs);
+  }
+};
+
+const HostNtt &ntt1() {
+  static HostNtt t(Q1, N1, 7);
+  return t;
+}
+const HostNtt &ntt2() {
+  static HostNtt t(Q2, N2, 22);
+  return t;
+}
+
+template <typename F>
+void parallel_for(size_t n, int nthreads, F f) {
+  if (nthreads <= 0)  // default: host cores, capped at 16 (the GPU box's CPU share)
+    nthreads = (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+  nthreads = (int)std::min<size_t>((size_t)nthreads, std::max<size_t>(1, n));
+  if (nthreads == 1) {
+    for (size_t i = 0; i < n; ++i) f(i);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (int t = 0; t < nthreads; ++t)
+    th.emplace_back([=, &f] {
+      for (size_t i = (size_t)t; i < n; i += (size_t)nthreads) f(i);
+    });
+  for (auto &x : th) x.join();
+}
+
+inline uint64_t to_mod(int64_t v, uint64_t q) {
+  int64_t r = v % (int64_t)q;
+  return (uint64_t)(r < 0 ? r + (int64_t)q : r);
+}
+
+}  // namespace
+}  // namespace omr
+
+// ==========================================================================================
+// SecretKeyPack (key_gen/secret.rs:17-95)
+// ==========================================================================================
+struct omr_secret_key_pack {
+  uint64_t seed;
+  uint8_t s0[omr::N0];     // clue LWE key, binary (LweSecretKeyType::Binary, mod.rs:44)
+  int8_t s1[omr::N1];      // first-level RLWE key, ternary (mod.rs:53)
+  uint8_t sint[omr::NI];   // intermediate LWE key, binary (mod.rs:72)
+  int8_t s2[omr::N2];      // second-level RLWE key, ternary (mod.rs:79)
+  uint16_t pk_a[omr::N0];  // RLWE-mode clue public key (LwePublicKeyRlweMode, secret.rs:99-107)
+  uint16_t pk_b[omr::N0];
+  std::vector<uint64_t> s1_ntt, s1_ntts, s2_ntt, s2_ntts;  // NTT(s) + Shoup companions
+};
+
+using namespace omr;
+
+extern "C" const char *omr_last_error(void) { return omr::g_last_error.c_str(); }
+extern "C" const char *omr_version(void) { return "omr_gpu 0.1 gfx950"; }
+
+extern "C" omr_status omr_keygen_secret(uint64_t seed, omr_secret_key_pack **out) {
+  if (!out) return set_error(OMR_ERR_INVALID_ARGUMENT, "omr_keygen_secret: out is NULL");
+  auto sk = std::make_unique<omr_secret_key_pack>();
+  sk->seed = seed;
+  {
+    Stream s(seed, DOM_S0, 0);
+    for (int i = 0; i < N0; ++i) sk->s0[i] = (uint8_t)s.bit();
+  }
+  {
+    Stream s(seed, DOM_S1, 0);
+    for (int i = 0; i < N1; ++i) sk->s1[i] = (int8_t)s.ternary();
+  }
+  {
+    Stream s(seed, DOM_SINT, 0);
+    for (int i = 0; i < NI; ++i) sk->sint[i] = (uint8_t)s.bit();
+  }
+  {
+    Stream s(seed, DOM_S2, 0);
+    for (int i = 0; i < N2; ++i) sk->s2[i] = (int8_t)s.ternary();
+  }
+  {  // public key: B = A * s0 + E over Z_2048[X]/(X^512+1)
+    Stream sa(seed, DOM_PK_A, 0), se(seed, DOM_PK_E, 0);
+    Gaussian g(SIGMA_CLUE);
+    int32_t b[N0];
+    for (int i = 0; i < N0; ++i) sk->pk_a[i] = (uint16_t)(sa.next32() & (Q0 - 1));
+    for (int i = 0; i < N0; ++i) b[i] = (int32_t)g.sample(se);
+    for (int t = 0; t < N0; ++t) {
+      if (!sk->s0[t]) continue;
+      for (int i = 0; i < N0; ++i) {
+        int e = i + t;
+        if (e < N0) b[e] += sk->pk_a[i];
+        else b[e - N0] -= sk->pk_a[i];
+      }
+    }
+    for (int i = 0; i < N0; ++i) sk->pk_b[i] = (uint16_t)(((b[i] % Q0) + Q0) % Q0);
+  }
+  auto ntt_of = [](const int8_t *s, int N, uint64_t q, const auto &tab, std::vector<uint64_t> &v,
+                   std::vector<uint64_t> &vs) {
+    v.resize(N);
+    vs.resize(N);
+    for (int i = 0; i < N; ++i) v[i] = to_mod(s[i], q);
+    tab.fwd(v.data());
+    for (int i = 0; i < N; ++i) vs[i] = tab.pre(v[i]);
+  };
+  ntt_of(sk->s1, N1, Q1, ntt1(), sk->s1_ntt, sk->s1_ntts);
+  ntt_of(sk->s2, N2, Q2, ntt2(), sk->s2_ntt, sk->s2_ntts);
+  *out = sk.release();
+  return OMR_OK;
+}
+
+extern "C" void omr_secret_destroy(omr_secret_key_pack *sk) { delete sk; }
+
+extern "C" omr_status omr_secret_export(const omr_secret_key_pack *sk, uint8_t *s0, int8_t *s1,
+                                        uint8_t *s_int, int8_t *s2) {
+  if (!sk) return set_error(OMR_ERR_INVALID_ARGUMENT, "omr_secret_export: sk is NULL");
+  if (s0) memcpy(s0, sk->s0, sizeof(sk->s0));
+  if (s1) memcpy(s1, sk->s1, sizeof(sk->s1));
+  if (s_int) memcpy(s_int, sk->sint, sizeof(sk->sint));
+  if (s2) memcpy(s2, sk->s2, sizeof(sk->s2));
+  return OMR_OK;
+}
+
+namespace omr {
+namespace {
+// RLWE encryption of zero with mask alpha, plus m*g in component `comp` of coefficient 0:
+// row = (alpha + [comp==0] m g, alpha*s + e + [comp==1] m g). Writes canonical residues.
+template <typename T>
+void ggsw_row(Stream &st, const Gaussian &gauss, const HostNtt &tab, const std::vector<uint64_t> &s_ntt,
+              const std::vector<uint64_t> &s_ntts, uint64_t mg, int comp, T *out_a, T *out_b,
+              const int8_t *sigma_s = nullptr, uint64_t sigma_scale = 0) {
+  const int N = tab.N;
+  const uint64_t q = tab.q;
+  std::vector<uint64_t> a(N), t(N);
+  for (int j = 0; j < N; ++j) a[j] = st.uniform(q);
+  for (int j = 0; j < N; ++j) t[j] = a[j];
+  tab.fwd(t.data());
+  for (int j = 0; j < N; ++j) t[j] = tab.mul(t[j], s_ntt[j], s_ntts[j]);
+  tab.inv(t.data());  // alpha * s
+  for (int j = 0; j < N; ++j) {
+    uint64_t b = t[j] + to_mod(gauss.sample(st), q);
+    b = b >= q ? b - q : b;
+    if (sigma_s && sigma_s[j]) {  // - sigma_g(s) * scale
+      uint64_t c = mulmod(sigma_scale, (uint64_t)(sigma_s[j] < 0 ? q - 1 : 1), q);
+      b = b >= c ? b - c : b + q - c;
+    }
+    t[j] = b;
+  }
+  if (mg) {
+    if (comp == 0) a[0] = (a[0] + mg) % q;
+    else t[0] = (t[0] + mg) % q;
+  }
+  for (int j = 0; j < N; ++j) {
+    out_a[j] = (T)a[j];
+    out_b[j] = (T)t[j];
+  }
+}
+}  // namespace
+}  // namespace omr
+
+// DetectionKey (key_gen/secret.rs:118-178).
+extern "C" omr_status omr_keygen_detection_key(const omr_secret_key_pack *sk, uint64_t seed,
+                                               uint32_t *bsk1, uint32_t *ksk, uint64_t *bsk2,
+                                               uint64_t *tk, int nthreads) {
+  if (!sk || !bsk1 || !ksk || !bsk2 || !tk)
+    return set_error(OMR_ERR_INVALID_ARGUMENT, "omr_keygen_detection_key: NULL argument");
+  const Gaussian g1(SIGMA_BR1), gks(SIGMA_KS), g2(SIGMA_BR2), gt(SIGMA_TRACE);
+  // BSK1: BlindRotationKey::generate(s0, NTT(s1), basis(q1,5,4), sigma 3.1859), :124-131
+  parallel_for((size_t)N0 * 2 * D1, nthreads, [&](size_t row) {
+    const size_t i = row / (2 * D1);
+    const int r = (int)(row % (2 * D1));
+    Stream st(seed, DOM_BSK1, row);
+    const int k = r < D1 ? r : r - D1;
+    const uint64_t mg = sk->s0[i] ? (1ull << (DROP1 + k * LOGB1)) : 0;
+    uint32_t *o = bsk1 + row * 2 * N1;
+    ggsw_row<uint32_t>(st, g1, ntt1(), sk->s1_ntt, sk->s1_ntts, mg, r < D1 ? 0 : 1, o, o + N1);
+  });
+  // KSK: NonPowOf2LweKeySwitchingKey::generate(s1 (-1 -> q1-1), s_int, ...), :133-147
+  parallel_for((size_t)N1 * KS_DIGITS, nthreads, [&](size_t row) {
+    const size_t i = row / KS_DIGITS;
+    const int j = (int)(row % KS_DIGITS);
+    Stream st(seed, DOM_KSK, row);
+    uint32_t *o = ksk + row * (NI + 1);
+    uint64_t b = 0;
+    for (int c = 0; c < NI; ++c) {
+      uint64_t a = st.uniform(Q1);
+      o[c] = (uint32_t)a;
+      if (sk->sint[c]) b += a;
+    }
+    b %= Q1;
+    b = (b + to_mod(gks.sample(st), Q1)) % Q1;
+    const uint64_t m = mulmod(to_mod(sk->s1[i], Q1), (1ull << j) % Q1, Q1);
+    o[NI] = (uint32_t)((b + m) % Q1);
+  });
+  // BSK2: BlindRotationKey::generate(s_int, NTT(s2), basis(q2,7,6), sigma 0.3908), :149-156
+  parallel_for((size_t)NI * 2 * D2, nthreads, [&](size_t row) {
+    const size_t i = row / (2 * D2);
+    const int r = (int)(row % (2 * D2));
+    Stream st(seed, DOM_BSK2, row);
+    const int k = r < D2 ? r : r - D2;
+    const uint64_t mg = sk->sint[i] ? (1ull << (DROP2 + k * LOGB2)) : 0;
+    uint64_t *o = bsk2 + row * 2 * N2;
+    ggsw_row<uint64_t>(st, g2, ntt2(), sk->s2_ntt, sk->s2_ntts, mg, r < D2 ? 0 : 1, o, o + N2);
+  });
+  // TraceKey::new(s2, NTT(s2), basis(q2,2,None), sigma 0.3908), :158-165
+  parallel_for((size_t)TRACE_STEPS * DT, nthreads, [&](size_t row) {
+    const int k = (int)(row / DT), j = (int)(row % DT);
+    const uint32_t g = (uint32_t)(N2 >> k) + 1;
+    int8_t sg[N2];
+    for (int i = 0; i < N2; ++i) {
+      uint32_t e = (uint32_t)(((uint64_t)i * g) % (2 * N2));
+      if (e < (uint32_t)N2) sg[e] = sk->s2[i];
+      else sg[e - N2] = (int8_t)-sk->s2[i];
+    }
+    Stream st(seed, DOM_TK, row);
+    uint64_t *o = tk + row * 2 * N2;
+    ggsw_row<uint64_t>(st, gt, ntt2(), sk->s2_ntt, sk->s2_ntts, 0, 1, o, o + N2, sg,
+                       (1ull << (2 * j)) % Q2);
+  });
+  return OMR_OK;
+}
+
+// Sender::gen_clues: ClueKey::gen_clues -> LwePublicKeyRlweMode::encrypt_multi_messages(&[0;7]).
+// u = A*r + e1, v = B*r + e2 (+ Delta*m = 0), r binary; clue = (u, v[0..7]).
+extern "C" omr_status omr_gen_clues(const omr_secret_key_pack *sk, uint64_t seed, uint64_t first,
+                                    size_t count, uint16_t *clue_a, uint16_t *clue_b,
+                                    int nthreads) {
+  if (!sk || !clue_a || !clue_b)
+    return set_error(OMR_ERR_INVALID_ARGUMENT, "omr_gen_clues: NULL argument");
+  const Gaussian g(SIGMA_CLUE);
+  parallel_for(count, nthreads, [&](size_t m) {
+    Stream st(seed, DOM_CLUE, first + m);
+    uint8_t r[N0];
+    for (int w = 0; w < N0 / 32; ++w) {
+      uint32_t v = st.next32();
+      for (int b = 0; b < 32; ++b) r[w * 32 + b] = (uint8_t)((v >> b) & 1u);
+    }
+    int32_t u[N0];
+    for (int i = 0; i < N0; ++i) u[i] = (int32_t)g.sample(st);
+    for (int t = 0; t < N0; ++t) {
+      if (!r[t]) continue;
+      const uint16_t *A = sk->pk_a;
+      for (int i = 0; i < N0 - t; ++i) u[i + t] += A[i];
+      for (int i = N0 - t; i < N0; ++i) u[i + t - N0] -= A[i];
+    }
+    uint16_t *ca = clue_a + m * N0;
+    for (int i = 0; i < N0; ++i) ca[i] = (uint16_t)(((u[i] % Q0) + Q0) % Q0);
+    for (int i = 0; i < CLUES; ++i) {
+      int32_t v = (int32_t)g.sample(st);
+      for (int t = 0; t <= i; ++t)
+        if (r[t]) v += sk->pk_b[i - t];
+      for (int t = i + 1; t < N0; ++t)
+        if (r[t]) v -= sk->pk_b[N0 + i - t];
+      clue_b[m * CLUES + i] = (uint16_t)(((v % Q0) + Q0) % Q0);
+    }
+  });
+  return OMR_OK;
+}
+
+extern "C" omr_status omr_get_retrieval_params(size_t all, size_t pertinent,
+                                               omr_retrieval_params *rp) {
+  if (!rp || all == 0) return set_error(OMR_ERR_INVALID_ARGUMENT, "omr_get_retrieval_params");
+  uint32_t pw = 0;
+  uint64_t acc = 1;
+  while (acc * (uint64_t)P <= all) {
+    acc *= (uint64_t)P;
+    ++pw;
+  }
+  if (acc < all) ++pw;
+  if (pw == 0) pw = 1;
+  rp->index_slots_per_bucket = pw;
+  rp->slots_per_bucket = pw + 1;
+  rp->slots_per_segment = rp->slots_per_bucket * BUCKETS;
+  rp->segment_per_cipher = N2 / rp->slots_per_segment;
+  rp->max_encode_indices_cipher_count = SEGMENTS / rp->segment_per_cipher;
+  rp->combination_count = (uint32_t)pertinent + 5;  // non-power-of-two p (retrieval_params.rs:85-89)
+  rp->cmb_count_per_cipher = 2;
+  rp->cmb_cipher_count = (rp->combination_count + 1) / 2;
+  return OMR_OK;
+}
+
+extern "C" omr_status omr_payload_weights(const uint8_t seed[32], size_t all, uint32_t combos,
+                                          uint32_t n_ct, uint32_t per_ct, uint16_t *out) {
+  if (!seed || !out || (size_t)n_ct * per_ct < combos)
+    return set_error(OMR_ERR_INVALID_ARGUMENT, "omr_payload_weights");
+  uint32_t key[8];
+  for (int i = 0; i < 8; ++i)
+    key[i] = (uint32_t)seed[4 * i] | ((uint32_t)seed[4 * i + 1] << 8) |
+             ((uint32_t)seed[4 * i + 2] << 16) | ((uint32_t)seed[4 * i + 3] << 24);
+  const size_t count = (size_t)combos * all;
+  uint32_t buf[16];
+  uint64_t block = 0;
+  int pos = 16;
+  size_t n = 0;
+  while (n < count) {
+    if (pos == 16) {
+      chacha_block(12, key, block++, 0, buf);
+      pos = 0;
+    }
+    const uint64_t m = (uint64_t)buf[pos++] * (uint64_t)P;
+    if ((uint32_t)m > 0xFFFFFFFEu) continue;  // UniformInt<u16> rejection zone
+    out[n++] = (uint16_t)(m >> 32);
+  }
+  memset(out + count, 0, ((size_t)n_ct * per_ct * all - count) * sizeof(uint16_t));
+  return OMR_OK;
+}

@@ -1,0 +1,328 @@
+"""Python host mirror of omr_core's public API over libomr_gpu.so (include/omr_gpu.h).
+
+Names follow the reference (omr_core/src/lib.rs:21-31): KeyGen, SecretKeyPack, DetectionKey,
+Detector (detect / detect_with_time_info / encode_pertinent_indices /
+encode_pertinent_payloads), RetrievalParams, Payload helpers. Every compute call goes through
+the HIP C ABI; there is no CPU fallback: if libomr_gpu.so is missing this module raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("OMR_GPU_LIB", os.path.join(HERE, "libomr_gpu.so"))
+
+N0, CLUE_COUNT, N1, NI, N2 = 512, 7, 1024, 670, 2048
+Q1, Q2, P = 134215681, 1125899906826241, 257
+KS_DIGITS, TRACE_STEPS, TRACE_DIGITS, PAYLOAD_LENGTH = 27, 11, 25, 612
+BSK1_SHAPE = (N0, 8, 2, N1)
+KSK_SHAPE = (N1, KS_DIGITS, NI + 1)
+BSK2_SHAPE = (NI, 12, 2, N2)
+TK_SHAPE = (TRACE_STEPS, TRACE_DIGITS, 2, N2)
+
+_u64p = np.ctypeslib.ndpointer(dtype=np.uint64, flags="C_CONTIGUOUS")
+_u32p = np.ctypeslib.ndpointer(dtype=np.uint32, flags="C_CONTIGUOUS")
+_u16p = np.ctypeslib.ndpointer(dtype=np.uint16, flags="C_CONTIGUOUS")
+_u8p = np.ctypeslib.ndpointer(dtype=np.uint8, flags="C_CONTIGUOUS")
+_i8p = np.ctypeslib.ndpointer(dtype=np.int8, flags="C_CONTIGUOUS")
+
+
+class OmrError(RuntimeError):
+    pass
+
+
+class _RetrievalParams(C.Structure):
+    _fields_ = [(n, C.c_uint32) for n in (
+        "index_slots_per_bucket", "slots_per_bucket", "slots_per_segment", "segment_per_cipher",
+        "max_encode_indices_cipher_count", "combination_count", "cmb_count_per_cipher", "cmb_cipher_count")]
+
+
+class _KeyView(C.Structure):
+    _fields_ = [("bsk1", C.c_void_p), ("ksk", C.c_void_p), ("bsk2", C.c_void_p), ("trace_key", C.c_void_p)]
+
+
+class _Timing(C.Structure):
+    _fields_ = [("total_ms", C.c_float), ("first_level_ms", C.c_float), ("key_switch_ms", C.c_float),
+                ("second_level_ms", C.c_float), ("messages", C.c_size_t)]
+
+
+EXPORTS = {
+    "omr_last_error": (C.c_char_p, []),
+    "omr_version": (C.c_char_p, []),
+    "omr_keygen_secret": (C.c_int, [C.c_uint64, C.POINTER(C.c_void_p)]),
+    "omr_secret_destroy": (None, [C.c_void_p]),
+    "omr_secret_export": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "omr_keygen_detection_key": (C.c_int, [C.c_void_p, C.c_uint64, _u32p, _u32p, _u64p, _u64p, C.c_int]),
+    "omr_gen_clues": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64, C.c_size_t, _u16p, _u16p, C.c_int]),
+    "omr_get_retrieval_params": (C.c_int, [C.c_size_t, C.c_size_t, C.POINTER(_RetrievalParams)]),
+    "omr_payload_weights": (C.c_int, [_u8p, C.c_size_t, C.c_uint32, C.c_uint32, C.c_uint32, _u16p]),
+    "omr_ctx_create": (C.c_int, [C.POINTER(_KeyView), C.c_int, C.POINTER(C.c_void_p)]),
+    "omr_ctx_destroy": (None, [C.c_void_p]),
+    "omr_ctx_set_batch": (C.c_int, [C.c_void_p, C.c_size_t]),
+    "omr_detect_batch": (C.c_int, [C.c_void_p, _u16p, _u16p, C.c_size_t, _u64p]),
+    "omr_detect_batch_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p]),
+    "omr_ctx_enable_timing": (C.c_int, [C.c_void_p, C.c_int]),
+    "omr_last_timing": (C.c_int, [C.c_void_p, C.POINTER(_Timing)]),
+    "omr_encode_indices": (C.c_int, [C.c_void_p, _u64p, C.c_size_t, C.c_size_t, C.c_size_t, C.c_uint64,
+                                     C.c_uint32, _u64p]),
+    "omr_encode_indices_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_size_t, C.c_size_t,
+                                            C.c_uint64, C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p]),
+    "omr_encode_payloads": (C.c_int, [C.c_void_p, _u64p, _u16p, C.c_size_t, C.c_size_t, C.c_size_t, _u16p,
+                                      C.c_uint32, C.c_uint32, _u64p]),
+    "omr_encode_payloads_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_size_t,
+                                             C.c_size_t, C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p,
+                                             C.c_void_p]),
+    "omr_first_level": (C.c_int, [C.c_void_p, _u16p, _u16p, C.c_size_t, _u32p]),
+    "omr_blind_rotate_level1": (C.c_int, [C.c_void_p, _u16p, _u16p, C.c_size_t, _u64p]),
+    "omr_second_level": (C.c_int, [C.c_void_p, _u32p, C.c_size_t, _u64p]),
+    "omr_blind_rotate_level2": (C.c_int, [C.c_void_p, _u32p, C.c_size_t, _u64p]),
+    "omr_ntt": (C.c_int, [C.c_int, C.c_int, _u64p, C.c_size_t, C.c_int]),
+}
+
+_lib = None
+
+
+def lib():
+    """Load libomr_gpu.so (fails loudly: there is no CPU path)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise OmrError(f"{LIB_PATH} not found: build it with `make -C tfhe-omr_amd` "
+                           "(or __graft_entry__.build())")
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in EXPORTS.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _check(st: int, what: str) -> None:
+    if st != 0:
+        raise OmrError(f"{what} failed ({st}): {lib().omr_last_error().decode()}")
+
+
+@dataclass
+class RetrievalParams:
+    """RetrievalParams::new(257, 2048, all, pertinent, 130, 25, 2) (retrieval_params.rs:50-106)."""
+    all_payloads_count: int
+    pertinent_count: int
+    index_slots_per_bucket: int = 0
+    slots_per_bucket: int = 0
+    slots_per_segment: int = 0
+    segment_per_cipher: int = 0
+    max_encode_indices_cipher_count: int = 0
+    combination_count: int = 0
+    cmb_count_per_cipher: int = 0
+    cmb_cipher_count: int = 0
+
+    def __post_init__(self):
+        rp = _RetrievalParams()
+        _check(lib().omr_get_retrieval_params(self.all_payloads_count, self.pertinent_count, C.byref(rp)),
+               "omr_get_retrieval_params")
+        for n, _ in _RetrievalParams._fields_:
+            setattr(self, n, getattr(rp, n))
+
+
+def payload_weights(seed: bytes, rp: RetrievalParams) -> np.ndarray:
+    """Seeded weights in the reference order (detector.rs:376-387): [n_ct*per_ct][all] u16."""
+    n = rp.cmb_cipher_count * rp.cmb_count_per_cipher * rp.all_payloads_count
+    out = np.zeros(n, dtype=np.uint16)
+    _check(lib().omr_payload_weights(np.frombuffer(bytes(seed), dtype=np.uint8).copy(), rp.all_payloads_count,
+                                     rp.combination_count, rp.cmb_cipher_count, rp.cmb_count_per_cipher, out),
+           "omr_payload_weights")
+    return out
+
+
+@dataclass
+class DetectionKey:
+    """Coefficient-domain evaluation keys (key_gen/detection.rs:9-16) in the ABI layout."""
+    bsk1: np.ndarray
+    ksk: np.ndarray
+    bsk2: np.ndarray
+    trace_key: np.ndarray
+
+    def size(self) -> int:
+        return sum(a.nbytes for a in (self.bsk1, self.ksk, self.bsk2, self.trace_key))
+
+
+class SecretKeyPack:
+    """KeyGen::generate_secret_key / SecretKeyPack (key_gen/secret.rs:46-209), seeded."""
+
+    def __init__(self, seed: int):
+        h = C.c_void_p()
+        _check(lib().omr_keygen_secret(seed, C.byref(h)), "omr_keygen_secret")
+        self._h = h
+        self.seed = seed
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().omr_secret_destroy(self._h)
+            self._h = None
+
+    def export(self):
+        s0 = np.zeros(N0, np.uint8)
+        s1 = np.zeros(N1, np.int8)
+        sint = np.zeros(NI, np.uint8)
+        s2 = np.zeros(N2, np.int8)
+        _check(lib().omr_secret_export(self._h, s0.ctypes.data, s1.ctypes.data, sint.ctypes.data,
+                                       s2.ctypes.data), "omr_secret_export")
+        return dict(s0=s0, s1=s1, s_int=sint, s2=s2)
+
+    def generate_detection_key(self, seed: int, nthreads: int = 0) -> DetectionKey:
+        bsk1 = np.empty(BSK1_SHAPE, np.uint32)
+        ksk = np.empty(KSK_SHAPE, np.uint32)
+        bsk2 = np.empty(BSK2_SHAPE, np.uint64)
+        tk = np.empty(TK_SHAPE, np.uint64)
+        _check(lib().omr_keygen_detection_key(self._h, seed, bsk1.reshape(-1), ksk.reshape(-1), bsk2.reshape(-1),
+                                              tk.reshape(-1), nthreads), "omr_keygen_detection_key")
+        return DetectionKey(bsk1, ksk, bsk2, tk)
+
+    def gen_clues(self, seed: int, first: int, count: int, nthreads: int = 0):
+        """Sender::gen_clues for global message indices [first, first+count)."""
+        a = np.empty((count, N0), np.uint16)
+        b = np.empty((count, CLUE_COUNT), np.uint16)
+        _check(lib().omr_gen_clues(self._h, seed, first, count, a.reshape(-1), b.reshape(-1), nthreads),
+               "omr_gen_clues")
+        return a, b
+
+
+class Detector:
+    """Detector (detector.rs:35-453) on one MI355X."""
+
+    def __init__(self, detection_key: DetectionKey, device: int = 0):
+        view = _KeyView(detection_key.bsk1.ctypes.data, detection_key.ksk.ctypes.data,
+                        detection_key.bsk2.ctypes.data, detection_key.trace_key.ctypes.data)
+        for a, shape, dt in ((detection_key.bsk1, BSK1_SHAPE, np.uint32), (detection_key.ksk, KSK_SHAPE, np.uint32),
+                             (detection_key.bsk2, BSK2_SHAPE, np.uint64), (detection_key.trace_key, TK_SHAPE, np.uint64)):
+            if a.shape != shape or a.dtype != dt or not a.flags.c_contiguous:
+                raise OmrError(f"detection key component has shape {a.shape} {a.dtype}, expected {shape} {dt}")
+        h = C.c_void_p()
+        _check(lib().omr_ctx_create(C.byref(view), device, C.byref(h)), "omr_ctx_create")
+        self._h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().omr_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    @property
+    def handle(self):
+        return self._h
+
+    def set_batch(self, batch: int):
+        _check(lib().omr_ctx_set_batch(self._h, batch), "omr_ctx_set_batch")
+
+    # detect (detector.rs:135) — one clue set -> NttRlweCiphertext [2][2048]
+    def detect(self, clue_a, clue_b) -> np.ndarray:
+        return self.detect_batch(np.asarray(clue_a).reshape(1, N0), np.asarray(clue_b).reshape(1, CLUE_COUNT))[0]
+
+    def detect_batch(self, clue_a, clue_b) -> np.ndarray:
+        clue_a = np.ascontiguousarray(clue_a, dtype=np.uint16)
+        clue_b = np.ascontiguousarray(clue_b, dtype=np.uint16)
+        D = clue_a.shape[0]
+        if clue_a.shape != (D, N0) or clue_b.shape != (D, CLUE_COUNT):
+            raise OmrError("clues must be u16 [D][512] and [D][7]")
+        out = np.empty((D, 2, N2), np.uint64)
+        _check(lib().omr_detect_batch(self._h, clue_a.reshape(-1), clue_b.reshape(-1), D, out.reshape(-1)),
+               "omr_detect_batch")
+        return out
+
+    def detect_batch_device(self, d_clue_a: int, d_clue_b: int, D: int, d_out: int, stream: int = 0):
+        _check(lib().omr_detect_batch_device(self._h, d_clue_a, d_clue_b, D, d_out, stream or None),
+               "omr_detect_batch_device")
+
+    def enable_timing(self, on: bool = True):
+        _check(lib().omr_ctx_enable_timing(self._h, int(on)), "omr_ctx_enable_timing")
+
+    def last_timing(self) -> dict:
+        t = _Timing()
+        _check(lib().omr_last_timing(self._h, C.byref(t)), "omr_last_timing")
+        return {n: getattr(t, n) for n, _ in _Timing._fields_}
+
+    # detect_with_time_info (detector.rs:169-221): stage split of one batch (device time)
+    def detect_with_time_info(self, clue_a, clue_b):
+        self.enable_timing(True)
+        out = self.detect_batch(clue_a, clue_b)
+        info = self.last_timing()
+        self.enable_timing(False)
+        return out, info
+
+    # encode_pertinent_indices (detector.rs:223-339)
+    def encode_pertinent_indices(self, rp: RetrievalParams, pertinency_vector, seed: int, ct: int = 0,
+                                 global_offset: int = 0) -> np.ndarray:
+        pv = np.ascontiguousarray(pertinency_vector, dtype=np.uint64)
+        D = pv.shape[0]
+        out = np.empty((2, N2), np.uint64)
+        _check(lib().omr_encode_indices(self._h, pv.reshape(-1), D, global_offset, rp.all_payloads_count, seed, ct,
+                                        out.reshape(-1)), "omr_encode_indices")
+        return out
+
+    # encode_pertinent_payloads (detector.rs:341-453)
+    def encode_pertinent_payloads(self, pertinency_vector, payloads, weights, rp: RetrievalParams,
+                                  global_offset: int = 0) -> np.ndarray:
+        pv = np.ascontiguousarray(pertinency_vector, dtype=np.uint64)
+        pay = np.ascontiguousarray(payloads, dtype=np.uint16)
+        w = np.ascontiguousarray(weights, dtype=np.uint16)
+        D = pv.shape[0]
+        n_ct, per = rp.cmb_cipher_count, rp.cmb_count_per_cipher
+        out = np.empty((n_ct, 2, N2), np.uint64)
+        _check(lib().omr_encode_payloads(self._h, pv.reshape(-1), pay.reshape(-1), D, global_offset,
+                                         rp.all_payloads_count, w, n_ct, per, out.reshape(-1)), "omr_encode_payloads")
+        return out
+
+    # ---- stage entry points (benches/two_level_bs.rs) ----
+    def first_level(self, clue_a, clue_b) -> np.ndarray:
+        clue_a = np.ascontiguousarray(clue_a, dtype=np.uint16).reshape(-1, N0)
+        clue_b = np.ascontiguousarray(clue_b, dtype=np.uint16).reshape(-1, CLUE_COUNT)
+        out = np.empty((clue_a.shape[0], NI + 1), np.uint32)
+        _check(lib().omr_first_level(self._h, clue_a.reshape(-1), clue_b.reshape(-1), clue_a.shape[0],
+                                     out.reshape(-1)), "omr_first_level")
+        return out
+
+    def blind_rotate_level1(self, lwe_a, lwe_b) -> np.ndarray:
+        lwe_a = np.ascontiguousarray(lwe_a, dtype=np.uint16).reshape(-1, N0)
+        lwe_b = np.ascontiguousarray(lwe_b, dtype=np.uint16).reshape(-1)
+        out = np.empty((lwe_a.shape[0], 2, N1), np.uint64)
+        _check(lib().omr_blind_rotate_level1(self._h, lwe_a.reshape(-1), lwe_b, lwe_a.shape[0], out.reshape(-1)),
+               "omr_blind_rotate_level1")
+        return out
+
+    def second_level(self, lwe_int) -> np.ndarray:
+        lwe = np.ascontiguousarray(lwe_int, dtype=np.uint32).reshape(-1, NI + 1)
+        out = np.empty((lwe.shape[0], 2, N2), np.uint64)
+        _check(lib().omr_second_level(self._h, lwe.reshape(-1), lwe.shape[0], out.reshape(-1)), "omr_second_level")
+        return out
+
+    def blind_rotate_level2(self, lwe_int) -> np.ndarray:
+        lwe = np.ascontiguousarray(lwe_int, dtype=np.uint32).reshape(-1, NI + 1)
+        out = np.empty((lwe.shape[0], 2, N2), np.uint64)
+        _check(lib().omr_blind_rotate_level2(self._h, lwe.reshape(-1), lwe.shape[0], out.reshape(-1)),
+               "omr_blind_rotate_level2")
+        return out
+
+
+def ntt(level: int, polys, inverse: bool = False, device: int = 0) -> np.ndarray:
+    p = np.array(polys, dtype=np.uint64, copy=True)
+    n = (1024 if level == 1 else 2048)
+    p2 = p.reshape(-1, n)
+    flat = np.ascontiguousarray(p2).reshape(-1)
+    _check(lib().omr_ntt(level, int(inverse), flat, p2.shape[0], device), "omr_ntt")
+    return flat.reshape(p.shape)
+
+
+class KeyGen:
+    """KeyGen::generate_secret_key (key_gen/mod.rs:21-27)."""
+
+    @staticmethod
+    def generate_secret_key(seed: int) -> SecretKeyPack:
+        return SecretKeyPack(seed)
