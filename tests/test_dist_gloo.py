@@ -1,0 +1,99 @@
+"""world_size-2 gloo test of the multi-GPU orchestration (tfhe-omr_amd/omr_dist.py) on CPU.
+The compute backend is the CPU oracle (test-only); the sharding, global offsets and the digest
+reduce are the production code. The 2-rank digest must equal the 1-rank digest bit-for-bit
+and decode to the pertinent indices and payloads (omr_time_analyze.rs:215-235)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+import product_lib as PL
+import retriever as R
+from product_lib import omr_amd as A
+
+import omr_dist
+
+TOTAL = 6
+MASK = np.array([0, 1, 0, 0, 1, 0], dtype=bool)
+INDEX_SEED = 77
+WSEED = bytes(range(5, 37))
+
+
+class OracleBackend:
+    def __init__(self, dk):
+        self.det = O.OracleDetector(dk.bsk1, dk.ksk, dk.bsk2, dk.trace_key)
+
+    def detect_batch(self, ca, cb):
+        return self.det.detect_batch(ca, cb, nthreads=2)
+
+    def encode_pertinent_indices(self, rp, pv, seed, ct, off):
+        return O.encode_indices(pv, off, rp.all_payloads_count, seed, ct)
+
+    def encode_pertinent_payloads(self, pv, payloads, w, rp, off):
+        return O.encode_payloads(pv, payloads, off, rp.all_payloads_count, w, rp.cmb_cipher_count,
+                                 rp.cmb_count_per_cipher)
+
+
+def shard_inputs(first, count):
+    a, b, _ = PL.keys()
+    ca, cb = a.gen_clues(500, first, count)
+    na, nb = b.gen_clues(501, first, count)
+    m = MASK[first:first + count]
+    ca[~m], cb[~m] = na[~m], nb[~m]
+    pay = np.stack([np.random.default_rng(1000 + g).integers(0, 256, 612) for g in range(first, first + count)])
+    return ca, cb, pay.astype(np.uint16)
+
+
+def _worker(rank, world, port, out_dir):
+    import torch.distributed as dist
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    _, _, dk = PL.keys()
+    rp = A.RetrievalParams(TOTAL, int(MASK.sum()))
+    w = A.payload_weights(WSEED, rp)
+    first, count = omr_dist.shard_range(rank, world, TOTAL)
+    ca, cb, pay = shard_inputs(first, count)
+    _, dg = omr_dist.run_omr_shard(OracleBackend(dk), ca, cb, pay, first, TOTAL, rp, INDEX_SEED, w, dist=dist)
+    if rank == 0:
+        np.savez(os.path.join(out_dir, f"digest_{world}.npz"), idx=dg.indices, pay=dg.payloads)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_shard_range_partitions():
+    for total in (1, 6, 65536, 2**20 + 3):
+        for world in (1, 2, 3, 8):
+            spans = [omr_dist.shard_range(r, world, total) for r in range(world)]
+            assert spans[0][0] == 0 and sum(c for _, c in spans) == total
+            assert all(spans[i][0] + spans[i][1] == spans[i + 1][0] for i in range(world - 1))
+
+
+@pytest.mark.slow
+def test_two_rank_digest_equals_one_rank(tmp_path):
+    import torch.multiprocessing as mp
+    PL.keys()  # build keys once in the parent (workers rebuild deterministically)
+    for world in (1, 2):
+        mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    d1 = np.load(tmp_path / "digest_1.npz")
+    d2 = np.load(tmp_path / "digest_2.npz")
+    assert np.array_equal(d1["idx"], d2["idx"]) and np.array_equal(d1["pay"], d2["pay"])
+    # the reduced digest decodes to the pertinent set and payloads
+    a, _, _ = PL.keys()
+    s2 = a.export()["s2"]
+    rp = A.RetrievalParams(TOTAL, int(MASK.sum()))
+    found = R.decode_indices(s2, d2["idx"], vars(rp), int(MASK.sum()))
+    assert found == set(np.nonzero(MASK)[0].tolist())
+    w = A.payload_weights(WSEED, rp)
+    _, _, pay = shard_inputs(0, TOTAL)
+    solved = R.decode_payloads(s2, d2["pay"], w, TOTAL, sorted(found), rp.combination_count)
+    for i, p in zip(sorted(found), solved):
+        assert p == pay[i].tolist()

@@ -74,7 +74,8 @@ std::vector<double> negacyclic_lut(const std::vector<uint64_t> &v, int N, int lo
 struct omr_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
-  double *bsk1 = nullptr, *bsk2 = nullptr, *tk = nullptr;
+  Key1T *bsk1 = nullptr;
+  double *bsk2 = nullptr, *tk = nullptr;
   uint32_t *ksk = nullptr;
   double *tables = nullptr;  // tw1 itw1 tw2 itw2 lut1 lut2
   uint16_t *trace_tabs = nullptr;
@@ -121,8 +122,8 @@ omr_status ensure_partial(omr_ctx *c, size_t elems) {
   return OMR_OK;
 }
 
-template <int LEVEL, typename IN>
-omr_status convert_keys(const IN *host, size_t npoly, double *dev, double scale, const double *tw,
+template <int LEVEL, typename IN, typename OUT>
+omr_status convert_keys(const IN *host, size_t npoly, OUT *dev, double scale, const double *tw,
                         hipStream_t st) {
   constexpr int N = Mod<LEVEL>::N;
   constexpr int T = LEVEL == 1 ? BR1_T : BR2_T;
@@ -132,7 +133,7 @@ omr_status convert_keys(const IN *host, size_t npoly, double *dev, double scale,
   for (size_t p0 = 0; p0 < npoly; p0 += chunk) {
     const size_t n = std::min(chunk, npoly - p0);
     HIP_TRY(hipMemcpyAsync(tmp, host + p0 * N, n * N * sizeof(IN), hipMemcpyHostToDevice, st));
-    key_to_ntt_kernel<LEVEL, IN><<<n, T, 0, st>>>(tmp, dev + p0 * N, n, scale, tw);
+    key_to_ntt_kernel<LEVEL, IN, OUT><<<n, T, 0, st>>>(tmp, dev + p0 * N, n, scale, tw);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(st));
   }
@@ -206,7 +207,7 @@ extern "C" omr_status omr_ctx_create(const omr_detection_key_view *key, int devi
   c->tb.trace_src = c->trace_tabs;
   c->tb.trace_perm = c->trace_tabs + TRACE_STEPS * N2;
   // keys
-  if (hipMalloc(&c->bsk1, BSK1_ELEMS * sizeof(double)) != hipSuccess ||
+  if (hipMalloc(&c->bsk1, BSK1_ELEMS * sizeof(Key1T)) != hipSuccess ||
       hipMalloc(&c->bsk2, BSK2_ELEMS * sizeof(double)) != hipSuccess ||
       hipMalloc(&c->tk, TK_ELEMS * sizeof(double)) != hipSuccess ||
       hipMalloc(&c->ksk, (KSK_ELEMS + 64) * sizeof(uint32_t)) != hipSuccess)
@@ -214,13 +215,13 @@ extern "C" omr_status omr_ctx_create(const omr_detection_key_view *key, int devi
   const double ninv1 = centred(h_powmod(N1, Q1 - 2, Q1), Q1);
   const double ninv2 = centred(h_powmod(N2, Q2 - 2, Q2), Q2);
   omr_status st;
-  if ((st = convert_keys<1, uint32_t>(key->bsk1, BSK1_ELEMS / N1, c->bsk1, ninv1, c->tb.tw1,
+  if ((st = convert_keys<1, uint32_t, Key1T>(key->bsk1, BSK1_ELEMS / N1, c->bsk1, ninv1, c->tb.tw1,
                                       c->stream)) != OMR_OK)
     return fail(st);
-  if ((st = convert_keys<2, uint64_t>(key->bsk2, BSK2_ELEMS / N2, c->bsk2, ninv2, c->tb.tw2,
+  if ((st = convert_keys<2, uint64_t, double>(key->bsk2, BSK2_ELEMS / N2, c->bsk2, ninv2, c->tb.tw2,
                                       c->stream)) != OMR_OK)
     return fail(st);
-  if ((st = convert_keys<2, uint64_t>(key->trace_key, TK_ELEMS / N2, c->tk, 1.0, c->tb.tw2,
+  if ((st = convert_keys<2, uint64_t, double>(key->trace_key, TK_ELEMS / N2, c->tk, 1.0, c->tb.tw2,
                                       c->stream)) != OMR_OK)
     return fail(st);
   scale_even_rows_kernel<<<(TK_ELEMS / N2 + 1) / 2, 256, 0, c->stream>>>(c->tk, TK_ELEMS / N2, ninv2);

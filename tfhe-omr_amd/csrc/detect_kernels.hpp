@@ -85,14 +85,41 @@ __device__ __forceinline__ double rot_read(const double *p, int j, int r) {
 // ------------------------------------------------------------------------------------------
 // One CMUX step of the binary blind rotation (BlindRotationKey::blind_rotate):
 //   ACC += ((X^a - 1) * ACC) [x] GGSW_i
-// acc_a/acc_b: coefficient domain, canonical, in LDS. ggsw: NTT-domain rows [2D][2][N],
-// pre-scaled by N^-1. All threads of the workgroup participate.
+// acc[p][e]: accumulator poly p (0 = mask, 1 = body), coefficient tid + e*T, canonical, held in
+// registers. xch: the workgroup's LDS buffer (N doubles) used for the rotation gather and the
+// NTT exchanges. tw/itw: twiddle tables (LDS copies). ggsw: NTT-domain rows [2D][2][N] of KeyT,
+// pre-scaled by N^-1. Digit rows are walked in one loop (row r = p*D + k) and key rows are
+// prefetched DEPTH rows ahead so their L2/MALL latency hides behind the transforms.
 // ------------------------------------------------------------------------------------------
-template <int LEVEL, int T, int E, int LOGB, int D, int DROP>
-__device__ __forceinline__ void cmux_step(double *acc_a, double *acc_b, double *xch, int a,
-                                          const double *__restrict__ ggsw,
-                                          const double *__restrict__ tw,
-                                          const double *__restrict__ itw, int tid) {
+template <typename KeyT, int E>
+struct KeyRow {
+  KeyT a[E], b[E];
+  __device__ __forceinline__ void load(const KeyT *__restrict__ row, int N, int off) {
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      a[e] = row[off + e];
+      b[e] = row[N + off + e];
+    }
+  }
+};
+
+// Stage poly `src` (registers, coefficient layout) into LDS and gather (X^a - 1) * src.
+template <class M, int T, int E>
+__device__ __forceinline__ void rotate_diff(const double (&src)[E], double *xch, int a, int tid,
+                                            double (&out)[E]) {
+  constexpr int N = M::N;
+#pragma unroll
+  for (int e = 0; e < E; ++e) xch[tid + e * T] = src[e];
+  __syncthreads();
+#pragma unroll
+  for (int e = 0; e < E; ++e) out[e] = canon_small<M>(rot_read<N>(xch, tid + e * T, a) - src[e]);
+  __syncthreads();
+}
+
+template <int LEVEL, int T, int E, int LOGB, int D, int DROP, typename KeyT, int DEPTH>
+__device__ __forceinline__ void cmux_step(double (&acc0)[E], double (&acc1)[E], double *xch, int a,
+                                          const KeyT *__restrict__ ggsw, const double *tw,
+                                          const double *itw, int tid) {
   using M = Mod<LEVEL>;
   using NTT = WgNtt<M, T, E>;
   using DG = Digits8<LOGB, D, DROP>;
@@ -100,36 +127,42 @@ __device__ __forceinline__ void cmux_step(double *acc_a, double *acc_b, double *
   double accA[E], accB[E];
 #pragma unroll
   for (int e = 0; e < E; ++e) accA[e] = accB[e] = 0.0;
+  KeyRow<KeyT, E> cur, nxt;
+  cur.load(ggsw, N, tid * E);
+  uint32_t pk[E][DG::DW];
 #pragma unroll 1
-  for (int p = 0; p < 2; ++p) {
-    const double *src = p ? acc_b : acc_a;
-    uint32_t pk[E][DG::DW];
+  for (int r = 0; r < 2 * D; ++r) {
+    if (DEPTH > 1 && r + 1 < 2 * D) nxt.load(ggsw + (size_t)(r + 1) * 2 * N, N, tid * E);
+    const int k = r < D ? r : r - D;
+    if (k == 0) {  // digits of (X^a - 1) * ACC_p, p = r / D
+      double src[E], v[E];
+#pragma unroll
+      for (int e = 0; e < E; ++e) src[e] = r == 0 ? acc0[e] : acc1[e];
+      rotate_diff<M, T, E>(src, xch, a, tid, v);
+#pragma unroll
+      for (int e = 0; e < E; ++e) DG::pack(v[e], pk[e]);
+    }
+    double x[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) x[e] = DG::get(pk[e], k);
+    NTT::fwd(x, xch, tw, tid);
 #pragma unroll
     for (int e = 0; e < E; ++e) {
-      const int j = tid + e * T;
-      const double v = canon_small<M>(rot_read<N>(src, j, a) - src[j]);
-      DG::pack(v, pk[e]);
+      accA[e] += mm<M>(x[e], (double)cur.a[e]);
+      accB[e] += mm<M>(x[e], (double)cur.b[e]);
     }
-#pragma unroll 1
-    for (int k = 0; k < D; ++k) {
-      double x[E];
-#pragma unroll
-      for (int e = 0; e < E; ++e) x[e] = DG::get(pk[e], k);
-      NTT::fwd(x, xch, tw, tid);
-      const double *ka = ggsw + (size_t)((p * D + k) * 2) * N + tid * E;
-      const double *kb = ka + N;
+    if (LEVEL == 2 && (k % 3) == 2) {
 #pragma unroll
       for (int e = 0; e < E; ++e) {
-        accA[e] += mm<M>(x[e], ka[e]);
-        accB[e] += mm<M>(x[e], kb[e]);
+        accA[e] = red<M>(accA[e]);
+        accB[e] = red<M>(accB[e]);
       }
-      if (LEVEL == 2 && (k % 3) == 2) {
-#pragma unroll
-        for (int e = 0; e < E; ++e) {
-          accA[e] = red<M>(accA[e]);
-          accB[e] = red<M>(accB[e]);
-        }
-      }
+    }
+    if (r + 1 < 2 * D) {
+      if (DEPTH > 1)
+        cur = nxt;
+      else
+        cur.load(ggsw + (size_t)(r + 1) * 2 * N, N, tid * E);
     }
   }
 #pragma unroll
@@ -139,30 +172,26 @@ __device__ __forceinline__ void cmux_step(double *acc_a, double *acc_b, double *
   }
   NTT::inv(accA, xch, itw, tid);
 #pragma unroll
-  for (int e = 0; e < E; ++e) {
-    const int j = tid + e * T;
-    acc_a[j] = canon<M>(acc_a[j] + accA[e]);
-  }
+  for (int e = 0; e < E; ++e) acc0[e] = canon<M>(acc0[e] + accA[e]);
   NTT::inv(accB, xch, itw, tid);
 #pragma unroll
-  for (int e = 0; e < E; ++e) {
-    const int j = tid + e * T;
-    acc_b[j] = canon<M>(acc_b[j] + accB[e]);
-  }
-  __syncthreads();
+  for (int e = 0; e < E; ++e) acc1[e] = canon<M>(acc1[e] + accB[e]);
 }
 
-// ACC = (0, X^{-b} * LUT)
+// ACC = (0, X^{-b} * LUT) in registers; copies the twiddle tables into LDS.
 template <int LEVEL, int T, int E>
-__device__ __forceinline__ void br_init(double *acc_a, double *acc_b, const double *lut, int b,
+__device__ __forceinline__ void br_init(double (&acc0)[E], double (&acc1)[E], const double *lut,
+                                        int b, double *tws, const double *tw, const double *itw,
                                         int tid) {
   constexpr int N = Mod<LEVEL>::N;
   const int r = (2 * N - (b % (2 * N))) % (2 * N);
 #pragma unroll
   for (int e = 0; e < E; ++e) {
     const int j = tid + e * T;
-    acc_a[j] = 0.0;
-    acc_b[j] = canon_small<Mod<LEVEL>>(rot_read<N>(lut, j, r));
+    acc0[e] = 0.0;
+    acc1[e] = canon_small<Mod<LEVEL>>(rot_read<N>(lut, j, r));
+    tws[j] = tw[j];
+    tws[N + j] = itw[j];
   }
   __syncthreads();
 }
@@ -174,17 +203,17 @@ __device__ __forceinline__ void br_init(double *acc_a, double *acc_b, const doub
 // Input is either a clue (lwe_a == nullptr: extract clue wg%7 of message wg/7, detector.rs:514)
 // or an explicit LWE (lwe_a [wg][512], lwe_b [wg]).
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(BR1_T) void br1_kernel(const uint16_t *__restrict__ clue_a,
+__global__ __launch_bounds__(BR1_T, BR1_WAVES) void br1_kernel(const uint16_t *__restrict__ clue_a,
                                                    const uint16_t *__restrict__ clue_b,
                                                    const uint16_t *__restrict__ lwe_a,
                                                    const uint16_t *__restrict__ lwe_b,
-                                                   const double *__restrict__ bsk1, DeviceTables tb,
+                                                   const Key1T *__restrict__ bsk1, DeviceTables tb,
                                                    uint32_t *__restrict__ ext,
                                                    uint64_t *__restrict__ rlwe_out, int mode) {
   using M = Mod<1>;
   constexpr int T = BR1_T, E = BR1_E, N = N1;
-  __shared__ double acc[2][N];
-  __shared__ double xch[WgNtt<M, T, E>::LDS_DOUBLES];
+  __shared__ double xch[N];
+  __shared__ double tws[2 * N];
   __shared__ uint16_t la[N0];
   const int tid = threadIdx.x;
   const size_t wg = blockIdx.x;
@@ -200,26 +229,32 @@ __global__ __launch_bounds__(BR1_T) void br1_kernel(const uint16_t *__restrict__
     for (int i = tid; i < N0; i += T) la[i] = lwe_a[wg * N0 + i] & (Q0 - 1);
     b = lwe_b[wg] & (Q0 - 1);
   }
-  br_init<1, T, E>(acc[0], acc[1], tb.lut1, b, tid);
+  double acc0[E], acc1[E];
+  br_init<1, T, E>(acc0, acc1, tb.lut1, b, tws, tb.tw1, tb.itw1, tid);
 #pragma unroll 1
   for (int i = 0; i < N0; ++i) {
     const int a = __builtin_amdgcn_readfirstlane(la[i]);
     if (a == 0) continue;  // (X^0 - 1) * ACC = 0
-    cmux_step<1, T, E, LOGB1, D1, DROP1>(acc[0], acc[1], xch, a,
-                                         bsk1 + (size_t)i * (2 * D1 * 2 * N), tb.tw1, tb.itw1, tid);
+    cmux_step<1, T, E, LOGB1, D1, DROP1, Key1T, OMR_KEY_DEPTH1>(
+        acc0, acc1, xch, a, bsk1 + (size_t)i * (2 * D1 * 2 * N), tws, tws + N, tid);
   }
-  if (mode == 0) {
+  if (mode == 0) {  // extract_lwe_locally (coefficient 0), detector.rs:561
+#pragma unroll
+    for (int e = 0; e < E; ++e) xch[tid + e * T] = acc0[e];
+    __syncthreads();
     uint32_t *o = ext + wg * (N + 1);
-    for (int j = tid; j < N; j += T) {
-      const double v = j == 0 ? acc[0][0] : -acc[0][N - j];  // extract_lwe_locally, :561
-      o[j] = (uint32_t)to_u64<M>(v);
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int j = tid + e * T;
+      o[j] = (uint32_t)to_u64<M>(j == 0 ? xch[0] : -xch[N - j]);
     }
-    if (tid == 0) o[N] = (uint32_t)to_u64<M>(acc[1][0]);
+    if (tid == 0) o[N] = (uint32_t)to_u64<M>(acc1[0]);
   } else {
     uint64_t *o = rlwe_out + wg * 2 * N;
-    for (int j = tid; j < N; j += T) {
-      o[j] = to_u64<M>(acc[0][j]);
-      o[N + j] = to_u64<M>(acc[1][j]);
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      o[tid + e * T] = to_u64<M>(acc0[e]);
+      o[N + tid + e * T] = to_u64<M>(acc1[e]);
     }
   }
 }
@@ -291,79 +326,87 @@ constexpr int KS_CT = 16;
 // one workgroup per message. mode 0: trace + NTT output u64 [wg][2][N2] (NttRlweCiphertext);
 // mode 1: blind rotation only, coefficient-domain output (stage test).
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(BR2_T) void br2_trace_kernel(const uint32_t *__restrict__ lwe_int,
-                                                         const double *__restrict__ bsk2,
+__global__ __launch_bounds__(BR2_T, BR2_WAVES) void br2_trace_kernel(const uint32_t *__restrict__ lwe_int,
+                                                         const Key2T *__restrict__ bsk2,
                                                          const double *__restrict__ tk,
                                                          DeviceTables tb,
                                                          uint64_t *__restrict__ out, int mode) {
   using M = Mod<2>;
   constexpr int T = BR2_T, E = BR2_E, N = N2;
   using NTT = WgNtt<M, T, E>;
-  __shared__ double acc[2][N];
-  __shared__ double xch[NTT::LDS_DOUBLES];
+  __shared__ double xch[N];
+  __shared__ double tws[2 * N];
   const int tid = threadIdx.x;
   const size_t wg = blockIdx.x;
   const uint32_t *lwe = lwe_int + wg * (NI + 1);
-  br_init<2, T, E>(acc[0], acc[1], tb.lut2, (int)lwe[NI], tid);
+  double acc0[E], acc1[E];
+  br_init<2, T, E>(acc0, acc1, tb.lut2, (int)lwe[NI], tws, tb.tw2, tb.itw2, tid);
+  const double *tw = tws, *itw = tws + N;
 #pragma unroll 1
   for (int i = 0; i < NI; ++i) {
     const int a = (int)__builtin_amdgcn_readfirstlane(lwe[i]) & (2 * N - 1);
     if (a == 0) continue;
-    cmux_step<2, T, E, LOGB2, D2, DROP2>(acc[0], acc[1], xch, a, bsk2 + (size_t)i * (2 * D2 * 2 * N),
-                                         tb.tw2, tb.itw2, tid);
+    cmux_step<2, T, E, LOGB2, D2, DROP2, Key2T, OMR_KEY_DEPTH2>(
+        acc0, acc1, xch, a, bsk2 + (size_t)i * (2 * D2 * 2 * N), tw, itw, tid);
   }
   uint64_t *o = out + wg * 2 * N;
   if (mode == 1) {
-    for (int j = tid; j < N; j += T) {
-      o[j] = to_u64<M>(acc[0][j]);
-      o[N + j] = to_u64<M>(acc[1][j]);
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      o[tid + e * T] = to_u64<M>(acc0[e]);
+      o[N + tid + e * T] = to_u64<M>(acc1[e]);
     }
     return;
   }
   // ---- hom_trace: c *= N^-1; for k: c += KS_k(sigma_g(c)); output NTT(c) ----
-  // a stays in the coefficient domain (acc[0]); b moves to the NTT domain (acc[1], index order).
+  // The mask stays in the coefficient domain (ca, layout tid + e*T); the body moves to the NTT
+  // domain (cb, layout tid*E + e) where sigma_g is an index permutation.
   constexpr double NINV = -549755813880.0;  // 2048^-1 mod q2 = 1125350151012361, centred (secret.rs:167-168)
-  {
-    double x[E];
+  double ca[E], cb[E];
 #pragma unroll
-    for (int e = 0; e < E; ++e) {
-      const int j = tid + e * T;
-      acc[0][j] = canon<M>(mm<M>(acc[0][j], NINV));
-      x[e] = canon<M>(mm<M>(acc[1][j], NINV));
-    }
-    NTT::fwd(x, xch, tb.tw2, tid);
-#pragma unroll
-    for (int e = 0; e < E; ++e) acc[1][tid * E + e] = canon<M>(x[e]);
-    __syncthreads();
+  for (int e = 0; e < E; ++e) {
+    ca[e] = canon<M>(mm<M>(acc0[e], NINV));
+    cb[e] = canon<M>(mm<M>(acc1[e], NINV));
   }
+  NTT::fwd(cb, xch, tw, tid);
+#pragma unroll
+  for (int e = 0; e < E; ++e) cb[e] = canon<M>(cb[e]);
 #pragma unroll 1
   for (int k = 0; k < TRACE_STEPS; ++k) {
     const uint16_t *src = tb.trace_src + k * N;
     const uint16_t *perm = tb.trace_perm + k * N;
     uint32_t pk[E][DigitsTrace::DW];
 #pragma unroll
+    for (int e = 0; e < E; ++e) xch[tid + e * T] = ca[e];
+    __syncthreads();
+#pragma unroll
     for (int e = 0; e < E; ++e) {
-      const int j = tid + e * T;
-      const int s = src[j];
-      const double v = s < N ? acc[0][s] : -acc[0][s - N];  // sigma_g(a)
-      DigitsTrace::pack(v, pk[e]);
+      const int s = src[tid + e * T];
+      DigitsTrace::pack(s < N ? xch[s] : -xch[s - N], pk[e]);  // sigma_g(a)
     }
+    __syncthreads();
     double accA[E], accB[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) accA[e] = accB[e] = 0.0;
     const double *key = tk + (size_t)k * DT * 2 * N;
 #pragma unroll 1
     for (int d = 0; d < DT; ++d) {
+      const double *ka = key + (size_t)(d * 2) * N + tid * E;  // alpha (pre-scaled by N^-1)
+      const double *kb = ka + N;                                 // beta (unscaled)
+      double kra[E], krb[E];
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        kra[e] = ka[e];
+        krb[e] = kb[e];
+      }
       double x[E];
 #pragma unroll
       for (int e = 0; e < E; ++e) x[e] = DigitsTrace::get(pk[e], d);
-      NTT::fwd(x, xch, tb.tw2, tid);
-      const double *ka = key + (size_t)(d * 2) * N + tid * E;  // alpha (pre-scaled by N^-1)
-      const double *kb = ka + N;                                 // beta (unscaled)
+      NTT::fwd(x, xch, tw, tid);
 #pragma unroll
       for (int e = 0; e < E; ++e) {
-        accA[e] += mm<M>(x[e], ka[e]);
-        accB[e] += mm<M>(x[e], kb[e]);
+        accA[e] += mm<M>(x[e], kra[e]);
+        accB[e] += mm<M>(x[e], krb[e]);
       }
       if ((d % 3) == 2) {
 #pragma unroll
@@ -374,37 +417,25 @@ __global__ __launch_bounds__(BR2_T) void br2_trace_kernel(const uint32_t *__rest
       }
     }
     // b_ntt += sigma_g(b)_ntt + B
-    double nb[E];
 #pragma unroll
-    for (int e = 0; e < E; ++e) {
-      const int t = tid * E + e;
-      nb[e] = acc[1][t] + acc[1][perm[t]] + red<M>(accB[e]);
-    }
+    for (int e = 0; e < E; ++e) xch[tid * E + e] = cb[e];
     __syncthreads();
 #pragma unroll
-    for (int e = 0; e < E; ++e) acc[1][tid * E + e] = canon<M>(nb[e]);
+    for (int e = 0; e < E; ++e) cb[e] = canon<M>(cb[e] + xch[perm[tid * E + e]] + red<M>(accB[e]));
+    __syncthreads();
     // a += INTT(A)
 #pragma unroll
     for (int e = 0; e < E; ++e) accA[e] = red<M>(accA[e]);
-    NTT::inv(accA, xch, tb.itw2, tid);
+    NTT::inv(accA, xch, itw, tid);
 #pragma unroll
-    for (int e = 0; e < E; ++e) {
-      const int j = tid + e * T;
-      acc[0][j] = canon<M>(acc[0][j] + accA[e]);
-    }
-    __syncthreads();
+    for (int e = 0; e < E; ++e) ca[e] = canon<M>(ca[e] + accA[e]);
   }
-  {
-    double x[E];
+  NTT::fwd(ca, xch, tw, tid);
 #pragma unroll
-    for (int e = 0; e < E; ++e) x[e] = acc[0][tid + e * T];
-    NTT::fwd(x, xch, tb.tw2, tid);
-#pragma unroll
-    for (int e = 0; e < E; ++e) {
-      const int t = tid * E + e;
-      o[t] = to_u64<M>(canon<M>(x[e]));
-      o[N + t] = to_u64<M>(acc[1][t]);
-    }
+  for (int e = 0; e < E; ++e) {
+    const int t = tid * E + e;
+    o[t] = to_u64<M>(canon<M>(ca[e]));
+    o[N + t] = to_u64<M>(cb[e]);
   }
 }
 

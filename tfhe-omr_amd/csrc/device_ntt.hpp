@@ -87,9 +87,11 @@ struct WgNtt {
   static constexpr int R = ilog2(E);
   static constexpr int NPASS = (L + R - 1) / R;
   static_assert(N == M::N, "NTT size mismatch");
-  static constexpr int LDS_DOUBLES = N + (N >> 5);
+  static constexpr int LDS_DOUBLES = N;
 
-  __device__ static __forceinline__ int pad(int j) { return j + (j >> 5); }
+  // XOR swizzle of the exchange buffer: bank-conflict free for every (T, E) used here
+  // (tools/lds_banks.py models the ds_read_b64 / ds_write_b64 lane groups).
+  __device__ static __forceinline__ int pad(int j) { return j ^ ((j >> R) & 31); }
 
   // Element index of register e in pass p (window of r stages starting at s0).
   __device__ static __forceinline__ int index(int p, int tid, int e) {

@@ -7,8 +7,44 @@
 namespace omr {
 
 // Workgroup geometry per level (T threads x E residues per thread = N).
-constexpr int BR1_T = 128, BR1_E = 8;    // N1 = 1024
-constexpr int BR2_T = 128, BR2_E = 16;   // N2 = 2048
+// Geometry / register targets chosen from measured variants:
+// level 1: 256 threads x 4 residues, >= 2 waves/SIMD; level 2: 256 x 8, 2 waves/SIMD.
+#ifndef BR1_WAVES
+#define BR1_WAVES 2
+#endif
+#ifndef BR2_WAVES
+#define BR2_WAVES 2
+#endif
+#ifndef BR1_TE
+#define BR1_TE 256, 4
+#endif
+#ifndef BR2_TE
+#define BR2_TE 256, 8
+#endif
+#ifndef OMR_KEY_DEPTH1
+#define OMR_KEY_DEPTH1 2  // level-1 key rows prefetched this many digits ahead (1 or 2)
+#endif
+#ifndef OMR_KEY_DEPTH2
+#define OMR_KEY_DEPTH2 1
+#endif
+#ifndef OMR_KEY_NT
+#define OMR_KEY_NT 0
+#endif
+constexpr int BR1_GEOM[2] = {BR1_TE};
+constexpr int BR2_GEOM[2] = {BR2_TE};
+constexpr int BR1_T = BR1_GEOM[0], BR1_E = BR1_GEOM[1];  // N1 = 1024
+constexpr int BR2_T = BR2_GEOM[0], BR2_E = BR2_GEOM[1];  // N2 = 2048
+
+// Device key element types: level 1 residues fit int32 (|x| <= (q1-1)/2), level 2 need FP64.
+#ifndef OMR_KEY1_DOUBLE
+#define OMR_KEY1_DOUBLE 0
+#endif
+#if OMR_KEY1_DOUBLE
+typedef double Key1T;
+#else
+typedef int32_t Key1T;
+#endif
+typedef double Key2T;
 constexpr int KS_MSGS = 64, KS_COLS = 64, KS_THREADS = 256;
 constexpr int ENC_T = 128, ENC_E = 16;
 
@@ -19,9 +55,9 @@ struct DeviceTables {
   const uint16_t *trace_src;              // [11][2048] coefficient source index of sigma_g (+N: negate)
 };
 
-// ---- key conversion: coefficient-domain canonical residues -> NTT-domain centred doubles ----
-template <int LEVEL, typename IN>
-__global__ void key_to_ntt_kernel(const IN *in, double *out, size_t npoly, double scale,
+// ---- key conversion: coefficient-domain canonical residues -> NTT-domain centred residues ----
+template <int LEVEL, typename IN, typename OUT>
+__global__ void key_to_ntt_kernel(const IN *in, OUT *out, size_t npoly, double scale,
                                   const double *tw) {
   using M = Mod<LEVEL>;
   constexpr int T = LEVEL == 1 ? BR1_T : BR2_T, E = LEVEL == 1 ? BR1_E : BR2_E;
@@ -35,9 +71,10 @@ __global__ void key_to_ntt_kernel(const IN *in, double *out, size_t npoly, doubl
 #pragma unroll
   for (int e = 0; e < E; ++e) x[e] = from_u64<M>((uint64_t)src[tid + e * T]);
   NTT::fwd(x, lds, tw, tid);
-  double *dst = out + poly * M::N + tid * E;
+  OUT *dst = out + poly * M::N + tid * E;
 #pragma unroll
-  for (int e = 0; e < E; ++e) dst[e] = scale == 1.0 ? canon<M>(x[e]) : canon<M>(mm<M>(canon<M>(x[e]), scale));
+  for (int e = 0; e < E; ++e)
+    dst[e] = (OUT)(scale == 1.0 ? canon<M>(x[e]) : canon<M>(mm<M>(canon<M>(x[e]), scale)));
 }
 
 // ---- plain NTT of canonical u64 polynomials (tests / omr_ntt) ----
