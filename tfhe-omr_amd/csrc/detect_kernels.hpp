@@ -178,6 +178,94 @@ __device__ __forceinline__ void cmux_step(double (&acc0)[E], double (&acc1)[E], 
   for (int e = 0; e < E; ++e) acc1[e] = canon<M>(acc1[e] + accB[e]);
 }
 
+// Paired variant: digit k of the mask and digit k of the body are transformed together
+// (two interleaved NTTs sharing every barrier), and the two inverse transforms likewise.
+// xch holds 2N doubles. MAC_EXACT (level 1 only): the transformed digit is reduced to
+// |x| <= q/2 + 2, so x*k is exact in FP64 (|x*k| < 2^52 for |k| <= (q1-1)/2) and two
+// products plus the running sum stay below 2^53; one reduction per two products.
+template <int LEVEL, int T, int E, int LOGB, int D, int DROP, typename KeyT, int DEPTH, bool MAC_EXACT>
+__device__ __forceinline__ void cmux_step_pair(double (&acc0)[E], double (&acc1)[E], double *xch,
+                                               int a, const KeyT *__restrict__ ggsw,
+                                               const double *tw, const double *itw, int tid) {
+  using M = Mod<LEVEL>;
+  using NTT = WgNtt<M, T, E>;
+  using DG = Digits8<LOGB, D, DROP>;
+  constexpr int N = M::N;
+  static_assert(!MAC_EXACT || LEVEL == 1, "exact-product MAC needs q < 2^27");
+  double acc[2][E];  // [0] = mask accumulator A, [1] = body accumulator B (NTT domain)
+#pragma unroll
+  for (int e = 0; e < E; ++e) acc[0][e] = acc[1][e] = 0.0;
+  uint32_t pk[2][E][DG::DW];
+  {  // digits of (X^a - 1) * ACC for both polys: one staging round trip
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      xch[tid + e * T] = acc0[e];
+      xch[N + tid + e * T] = acc1[e];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int j = tid + e * T;
+      DG::pack(canon_small<M>(rot_read<N>(xch, j, a) - acc0[e]), pk[0][e]);
+      DG::pack(canon_small<M>(rot_read<N>(xch + N, j, a) - acc1[e]), pk[1][e]);
+    }
+    __syncthreads();
+  }
+  // key rows: row k (mask digit k) and row D+k (body digit k), each [2][N] (A, B components)
+  KeyRow<KeyT, E> c0, c1, n0, n1;
+  c0.load(ggsw, N, tid * E);
+  c1.load(ggsw + (size_t)D * 2 * N, N, tid * E);
+#pragma unroll 1
+  for (int k = 0; k < D; ++k) {
+    if (DEPTH > 1 && k + 1 < D) {
+      n0.load(ggsw + (size_t)(k + 1) * 2 * N, N, tid * E);
+      n1.load(ggsw + (size_t)(D + k + 1) * 2 * N, N, tid * E);
+    }
+    double x[2][E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      x[0][e] = DG::get(pk[0][e], k);
+      x[1][e] = DG::get(pk[1][e], k);
+    }
+    NTT::template fwdC<2>(x, xch, tw, tid);
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      if constexpr (MAC_EXACT) {
+        const double x0 = red<M>(x[0][e]), x1 = red<M>(x[1][e]);
+        acc[0][e] = red<M>(__fma_rn(x1, (double)c1.a[e], __fma_rn(x0, (double)c0.a[e], acc[0][e])));
+        acc[1][e] = red<M>(__fma_rn(x1, (double)c1.b[e], __fma_rn(x0, (double)c0.b[e], acc[1][e])));
+      } else {
+        acc[0][e] += mm<M>(x[0][e], (double)c0.a[e]) + mm<M>(x[1][e], (double)c1.a[e]);
+        acc[1][e] += mm<M>(x[0][e], (double)c0.b[e]) + mm<M>(x[1][e], (double)c1.b[e]);
+        if (LEVEL == 2) {
+          acc[0][e] = red<M>(acc[0][e]);
+          acc[1][e] = red<M>(acc[1][e]);
+        }
+      }
+    }
+    if (k + 1 < D) {
+      if (DEPTH > 1) {
+        c0 = n0;
+        c1 = n1;
+      } else {
+        c0.load(ggsw + (size_t)(k + 1) * 2 * N, N, tid * E);
+        c1.load(ggsw + (size_t)(D + k + 1) * 2 * N, N, tid * E);
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    acc[0][e] = red<M>(acc[0][e]);
+    acc[1][e] = red<M>(acc[1][e]);
+  }
+  NTT::template invC<2>(acc, xch, itw, tid);
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    acc0[e] = canon<M>(acc0[e] + acc[0][e]);
+    acc1[e] = canon<M>(acc1[e] + acc[1][e]);
+  }
+}
+
 // ACC = (0, X^{-b} * LUT) in registers; copies the twiddle tables into LDS.
 template <int LEVEL, int T, int E>
 __device__ __forceinline__ void br_init(double (&acc0)[E], double (&acc1)[E], const double *lut,
@@ -212,7 +300,7 @@ __global__ __launch_bounds__(BR1_T, BR1_WAVES) void br1_kernel(const uint16_t *_
                                                    uint64_t *__restrict__ rlwe_out, int mode) {
   using M = Mod<1>;
   constexpr int T = BR1_T, E = BR1_E, N = N1;
-  __shared__ double xch[N];
+  __shared__ double xch[OMR_PAIR1 ? 2 * N : N];
   __shared__ double tws[2 * N];
   __shared__ uint16_t la[N0];
   const int tid = threadIdx.x;
@@ -235,8 +323,13 @@ __global__ __launch_bounds__(BR1_T, BR1_WAVES) void br1_kernel(const uint16_t *_
   for (int i = 0; i < N0; ++i) {
     const int a = __builtin_amdgcn_readfirstlane(la[i]);
     if (a == 0) continue;  // (X^0 - 1) * ACC = 0
+#if OMR_PAIR1
+    cmux_step_pair<1, T, E, LOGB1, D1, DROP1, Key1T, OMR_KEY_DEPTH1, OMR_MAC_EXACT1 != 0>(
+        acc0, acc1, xch, a, bsk1 + (size_t)i * (2 * D1 * 2 * N), tws, tws + N, tid);
+#else
     cmux_step<1, T, E, LOGB1, D1, DROP1, Key1T, OMR_KEY_DEPTH1>(
         acc0, acc1, xch, a, bsk1 + (size_t)i * (2 * D1 * 2 * N), tws, tws + N, tid);
+#endif
   }
   if (mode == 0) {  // extract_lwe_locally (coefficient 0), detector.rs:561
 #pragma unroll
@@ -334,7 +427,7 @@ __global__ __launch_bounds__(BR2_T, BR2_WAVES) void br2_trace_kernel(const uint3
   using M = Mod<2>;
   constexpr int T = BR2_T, E = BR2_E, N = N2;
   using NTT = WgNtt<M, T, E>;
-  __shared__ double xch[N];
+  __shared__ double xch[OMR_PAIR2 ? 2 * N : N];
   __shared__ double tws[2 * N];
   const int tid = threadIdx.x;
   const size_t wg = blockIdx.x;
@@ -346,8 +439,13 @@ __global__ __launch_bounds__(BR2_T, BR2_WAVES) void br2_trace_kernel(const uint3
   for (int i = 0; i < NI; ++i) {
     const int a = (int)__builtin_amdgcn_readfirstlane(lwe[i]) & (2 * N - 1);
     if (a == 0) continue;
+#if OMR_PAIR2
+    cmux_step_pair<2, T, E, LOGB2, D2, DROP2, Key2T, OMR_KEY_DEPTH2, false>(
+        acc0, acc1, xch, a, bsk2 + (size_t)i * (2 * D2 * 2 * N), tw, itw, tid);
+#else
     cmux_step<2, T, E, LOGB2, D2, DROP2, Key2T, OMR_KEY_DEPTH2>(
         acc0, acc1, xch, a, bsk2 + (size_t)i * (2 * D2 * 2 * N), tw, itw, tid);
+#endif
   }
   uint64_t *o = out + wg * 2 * N;
   if (mode == 1) {

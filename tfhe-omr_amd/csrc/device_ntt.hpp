@@ -28,7 +28,8 @@ struct Mod<2> {
   static constexpr double QINV = 1.0 / 1125899906826241.0;
   static constexpr double HALF = 562949953413120.0;
   static constexpr int N = N2, L = 11;
-  static constexpr int RED_FWD = 4, RED_INV = 3;  // stages between reductions
+  // stages between reductions; bounds checked in DESIGN.md §3 (worst intermediate 0.78 * 2^53)
+  static constexpr int RED_FWD = 6, RED_INV = 3;
 };
 
 // a*w mod q, |result| <= (0.5 + A/5) q for |a| <= A q, |w| <= q/2.
@@ -108,26 +109,33 @@ struct WgNtt {
     for (int e = 0; e < E; ++e) x[e] = red<M>(x[e]);
   }
 
-  __device__ static __forceinline__ void exchange(double (&x)[E], double *lds, int tid, int p_from,
-                                                  int p_to) {
+  // ---- C independent transforms interleaved (C x E residues per thread, C LDS buffers) ----
+  template <int C>
+  __device__ static __forceinline__ void exchangeC(double (&x)[C][E], double *lds, int tid,
+                                                   int p_from, int p_to) {
 #pragma unroll
-    for (int e = 0; e < E; ++e) lds[pad(index(p_from, tid, e))] = x[e];
+    for (int c = 0; c < C; ++c)
+#pragma unroll
+      for (int e = 0; e < E; ++e) lds[c * N + pad(index(p_from, tid, e))] = x[c][e];
     __syncthreads();
 #pragma unroll
-    for (int e = 0; e < E; ++e) x[e] = lds[pad(index(p_to, tid, e))];
+    for (int c = 0; c < C; ++c)
+#pragma unroll
+      for (int e = 0; e < E; ++e) x[c][e] = lds[c * N + pad(index(p_to, tid, e))];
     __syncthreads();
   }
 
-  template <int P>
-  __device__ static __forceinline__ void fwd_pass(double (&x)[E], const double *__restrict__ tw,
-                                                  int tid, int &since_red) {
+  template <int P, int C>
+  __device__ static __forceinline__ void fwd_passC(double (&x)[C][E], const double *tw, int tid,
+                                                   int &since_red) {
     constexpr int s0 = P * R;
     constexpr int r = (L - s0) < R ? (L - s0) : R;
     constexpr int lb = L - s0 - r;
 #pragma unroll
     for (int k = 0; k < r; ++k) {
       if (since_red >= M::RED_FWD) {
-        reduce_all(x);
+#pragma unroll
+        for (int c = 0; c < C; ++c) reduce_all(x[c]);
         since_red = 0;
       }
       const int s = s0 + k;
@@ -138,27 +146,30 @@ struct WgNtt {
         if (ep & half) continue;
         const int F = (tid << (R - r)) | (e >> r);
         const int hi = F >> lb;
-        const int ti = (1 << s) + ((hi << k) | (ep >> (r - k)));
-        const double w = tw[ti];
-        const double u = x[e];
-        const double v = mm<M>(x[e + half], w);
-        x[e] = u + v;
-        x[e + half] = u - v;
+        const double w = tw[(1 << s) + ((hi << k) | (ep >> (r - k)))];
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+          const double u = x[c][e];
+          const double v = mm<M>(x[c][e + half], w);
+          x[c][e] = u + v;
+          x[c][e + half] = u - v;
+        }
       }
       ++since_red;
     }
   }
 
-  template <int P>
-  __device__ static __forceinline__ void inv_pass(double (&x)[E], const double *__restrict__ itw,
-                                                  int tid, int &since_red) {
+  template <int P, int C>
+  __device__ static __forceinline__ void inv_passC(double (&x)[C][E], const double *itw, int tid,
+                                                   int &since_red) {
     constexpr int s0 = P * R;
     constexpr int r = (L - s0) < R ? (L - s0) : R;
     constexpr int lb = L - s0 - r;
 #pragma unroll
     for (int k = r - 1; k >= 0; --k) {
       if (since_red >= M::RED_INV) {
-        reduce_all(x);
+#pragma unroll
+        for (int c = 0; c < C; ++c) reduce_all(x[c]);
         since_red = 0;
       }
       const int s = s0 + k;
@@ -169,48 +180,58 @@ struct WgNtt {
         if (ep & half) continue;
         const int F = (tid << (R - r)) | (e >> r);
         const int hi = F >> lb;
-        const int ti = (1 << s) + ((hi << k) | (ep >> (r - k)));
-        const double w = itw[ti];
-        const double u = x[e];
-        const double v = x[e + half];
-        x[e] = u + v;
-        x[e + half] = mm<M>(u - v, w);
+        const double w = itw[(1 << s) + ((hi << k) | (ep >> (r - k)))];
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+          const double u = x[c][e];
+          const double v = x[c][e + half];
+          x[c][e] = u + v;
+          x[c][e + half] = mm<M>(u - v, w);
+        }
       }
       ++since_red;
     }
   }
 
-  template <int P>
-  __device__ static __forceinline__ void fwd_from(double (&x)[E], double *lds,
-                                                  const double *__restrict__ tw, int tid,
-                                                  int &since_red) {
+  template <int P, int C>
+  __device__ static __forceinline__ void fwd_fromC(double (&x)[C][E], double *lds, const double *tw,
+                                                   int tid, int &since_red) {
     if constexpr (P < NPASS) {
-      if constexpr (P > 0) exchange(x, lds, tid, P - 1, P);
-      fwd_pass<P>(x, tw, tid, since_red);
-      fwd_from<P + 1>(x, lds, tw, tid, since_red);
+      if constexpr (P > 0) exchangeC<C>(x, lds, tid, P - 1, P);
+      fwd_passC<P, C>(x, tw, tid, since_red);
+      fwd_fromC<P + 1, C>(x, lds, tw, tid, since_red);
     }
   }
-  template <int P>
-  __device__ static __forceinline__ void inv_from(double (&x)[E], double *lds,
-                                                  const double *__restrict__ itw, int tid,
-                                                  int &since_red) {
+  template <int P, int C>
+  __device__ static __forceinline__ void inv_fromC(double (&x)[C][E], double *lds, const double *itw,
+                                                   int tid, int &since_red) {
     if constexpr (P >= 0) {
-      if constexpr (P < NPASS - 1) exchange(x, lds, tid, P + 1, P);
-      inv_pass<P>(x, itw, tid, since_red);
-      inv_from<P - 1>(x, lds, itw, tid, since_red);
+      if constexpr (P < NPASS - 1) exchangeC<C>(x, lds, tid, P + 1, P);
+      inv_passC<P, C>(x, itw, tid, since_red);
+      inv_fromC<P - 1, C>(x, lds, itw, tid, since_red);
     }
   }
 
-  // Input bounds: forward |x| <= q/2 (small digits in practice); inverse |x| <= q/2.
-  __device__ static __forceinline__ void fwd(double (&x)[E], double *lds,
-                                             const double *__restrict__ tw, int tid) {
+  // C transforms at once; lds holds C*N doubles. Bounds as for the single transforms.
+  template <int C>
+  __device__ static __forceinline__ void fwdC(double (&x)[C][E], double *lds, const double *tw,
+                                              int tid) {
     int since_red = 0;
-    fwd_from<0>(x, lds, tw, tid, since_red);
+    fwd_fromC<0, C>(x, lds, tw, tid, since_red);
   }
-  __device__ static __forceinline__ void inv(double (&x)[E], double *lds,
-                                             const double *__restrict__ itw, int tid) {
+  template <int C>
+  __device__ static __forceinline__ void invC(double (&x)[C][E], double *lds, const double *itw,
+                                              int tid) {
     int since_red = 0;
-    inv_from<NPASS - 1>(x, lds, itw, tid, since_red);
+    inv_fromC<NPASS - 1, C>(x, lds, itw, tid, since_red);
+  }
+
+  // Single-transform API.
+  __device__ static __forceinline__ void fwd(double (&x)[E], double *lds, const double *tw, int tid) {
+    fwdC<1>(reinterpret_cast<double(&)[1][E]>(x), lds, tw, tid);
+  }
+  __device__ static __forceinline__ void inv(double (&x)[E], double *lds, const double *itw, int tid) {
+    invC<1>(reinterpret_cast<double(&)[1][E]>(x), lds, itw, tid);
   }
 };
 

@@ -22,10 +22,19 @@ namespace omr {
 #define BR2_TE 256, 8
 #endif
 #ifndef OMR_KEY_DEPTH1
-#define OMR_KEY_DEPTH1 2  // level-1 key rows prefetched this many digits ahead (1 or 2)
+#define OMR_KEY_DEPTH1 1  // level-1 key rows prefetched this many digits ahead (1 or 2)
 #endif
 #ifndef OMR_KEY_DEPTH2
 #define OMR_KEY_DEPTH2 1
+#endif
+#ifndef OMR_PAIR1
+#define OMR_PAIR1 1       // level 1: transform mask and body digits as interleaved pairs
+#endif
+#ifndef OMR_MAC_EXACT1
+#define OMR_MAC_EXACT1 1  // level 1: exact-product multiply-accumulate (one reduction per 2)
+#endif
+#ifndef OMR_PAIR2
+#define OMR_PAIR2 0       // level 2: paired mask/body digit transforms
 #endif
 #ifndef OMR_KEY_NT
 #define OMR_KEY_NT 0
