@@ -176,6 +176,11 @@ omr_status omr_first_level(omr_ctx *ctx, const uint16_t *clue_a, const uint16_t 
 /* One level-1 blind rotation per LWE (a u16 [n][512], b u16 [n]): out u64 [n][2][1024]. */
 omr_status omr_blind_rotate_level1(omr_ctx *ctx, const uint16_t *lwe_a, const uint16_t *lwe_b,
                                    size_t n, uint64_t *out);
+/* Negacyclic product a * k mod (X^1024 + 1, q1) of n pairs through the level-1 FFT external-
+ * product path (device_fft.hpp): a u32 [n][1024] with digit-sized centred values (|a| <= 17),
+ * k u32 [n][1024] canonical; out u64 [n][1024] canonical. */
+omr_status omr_fft1_mul(omr_ctx *ctx, const uint32_t *a, const uint32_t *k, size_t n,
+                        uint64_t *out);
 /* Second level + trace (detector.rs:599-639) on LWE(670, 4096) inputs: out u64 [n][2][2048]. */
 omr_status omr_second_level(omr_ctx *ctx, const uint32_t *lwe_int, size_t n, uint64_t *out);
 /* Level-2 blind rotation only (no trace): out u64 [n][2][2048] coefficient domain. */

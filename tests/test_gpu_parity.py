@@ -20,6 +20,34 @@ def prim():
         return json.load(f)
 
 
+def _negacyclic_mod_q1(d, k):
+    """Exact d * k mod (X^1024 + 1, q1) (int64 is exact: |d| <= 17, |k| < 2^27, 1024 terms)."""
+    full = np.convolve(d.astype(np.int64), k.astype(np.int64))
+    r = full[:1024].copy()
+    r[:1023] -= full[1024:]
+    return (r % A.Q1).astype(np.uint64)
+
+
+def test_gpu_fft1_product_exact():
+    """The level-1 FFT external product (device_fft.hpp) returns the exact integer product for
+    digit-sized inputs: random digits, and digits of maximal magnitude aligned with the key's
+    signs for one output coefficient (the worst case for rounding error)."""
+    a_sk, _, dk = PL.keys()
+    det = A.Detector(dk)
+    rng = np.random.default_rng(11)
+    q1 = A.Q1
+    keys = rng.integers(-(q1 - 1) // 2, (q1 - 1) // 2 + 1, (6, 1024))
+    digs = [rng.integers(-17, 18, 1024) for _ in range(3)]
+    for c in (0, 511, 1023):  # out_c = sum_j d_j * k_{c-j} (negated when wrapped)
+        k = keys[len(digs)]
+        t = (c - np.arange(1024)) % 1024
+        sign = np.where(np.arange(1024) <= c, 1, -1)
+        digs.append(17 * sign * np.sign(k[t]).astype(np.int64))
+    got = det.fft1_mul(np.stack([d % q1 for d in digs]).astype(np.uint32), (keys % q1).astype(np.uint32))
+    for i, d in enumerate(digs):
+        assert np.array_equal(got[i], _negacyclic_mod_q1(d, keys[i])), f"case {i}"
+
+
 @pytest.mark.parametrize("level", [1, 2])
 def test_gpu_ntt_matches_definition(prim, level):
     vecs = prim["ntt"][str(level)]

@@ -69,12 +69,34 @@ std::vector<double> negacyclic_lut(const std::vector<uint64_t> &v, int N, int lo
   return lut;
 }
 
+// Level-1 FFT twiddles (device_fft.hpp): tw[(1 << s) + i] = w^(eps(s, i) / 2), w = exp(i pi / 1024),
+// eps(0, 0) = 512, eps(s+1, 2i) = eps(s, i) / 2, eps(s+1, 2i+1) = eps(s, i) / 2 + 1024 (mod 2048).
+// Evaluated in long double and rounded once.
+std::vector<double2> fft1_twiddles() {
+  std::vector<double2> tw(512, make_double2(1.0, 0.0));
+  std::vector<int> eps{512};
+  for (int s = 0; s < 9; ++s) {
+    std::vector<int> next;
+    for (int i = 0; i < (1 << s); ++i) {
+      const int half = eps[i] / 2;
+      const long double ang = 3.14159265358979323846264338327950288L * (long double)half / 1024.0L;
+      tw[(1 << s) + i] = make_double2((double)cosl(ang), (double)sinl(ang));
+      next.push_back(half % 2048);
+      next.push_back((half + 1024) % 2048);
+    }
+    eps.swap(next);
+  }
+  return tw;
+}
+
 }  // namespace
 
 struct omr_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
-  Key1T *bsk1 = nullptr;
+  Key1T *bsk1 = nullptr;    // level-1 NTT-domain keys (OMR_FFT1 == 0)
+  double2 *bsk1f = nullptr; // level-1 FFT-domain keys (OMR_FFT1)
+  double2 *fft1 = nullptr;
   double *bsk2 = nullptr, *tk = nullptr;
   uint32_t *ksk = nullptr;
   double *tables = nullptr;  // tw1 itw1 tw2 itw2 lut1 lut2
@@ -138,6 +160,36 @@ omr_status convert_keys(const IN *host, size_t npoly, OUT *dev, double scale, co
     HIP_TRY(hipStreamSynchronize(st));
   }
   hipFree(tmp);
+  return OMR_OK;
+}
+
+omr_status convert_keys_fft1(const uint32_t *host, size_t npoly, double2 *dev, const double2 *tw,
+                             hipStream_t st) {
+  const size_t chunk = 4096;
+  uint32_t *tmp = nullptr;
+  HIP_TRY(hipMalloc(&tmp, chunk * N1 * sizeof(uint32_t)));
+  for (size_t p0 = 0; p0 < npoly; p0 += chunk) {
+    const size_t n = std::min(chunk, npoly - p0);
+    HIP_TRY(hipMemcpyAsync(tmp, host + p0 * N1, n * N1 * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+    key_to_fft1_kernel<<<n, 64, 0, st>>>(tmp, dev + p0 * Fft512::N, n, tw);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(st));
+  }
+  hipFree(tmp);
+  return OMR_OK;
+}
+
+// Level-1 blind rotations: n workgroups (mode 0: clue wg%7 of message wg/7 -> extracted LWE;
+// mode 1: explicit LWEs -> full RLWE).
+omr_status launch_br1(omr_ctx *c, size_t n, const uint16_t *ca, const uint16_t *cb,
+                      const uint16_t *la, const uint16_t *lb, uint32_t *ext, uint64_t *rlwe, int mode,
+                      hipStream_t st) {
+#if OMR_FFT1
+  br1f_kernel<<<(unsigned)n, 64, 0, st>>>(ca, cb, la, lb, c->bsk1f, c->tb, ext, rlwe, mode);
+#else
+  br1_kernel<<<(unsigned)n, BR1_T, 0, st>>>(ca, cb, la, lb, c->bsk1, c->tb, ext, rlwe, mode);
+#endif
+  HIP_TRY(hipGetLastError());
   return OMR_OK;
 }
 
@@ -206,8 +258,15 @@ extern "C" omr_status omr_ctx_create(const omr_detection_key_view *key, int devi
   c->tb.lut2 = c->tables + 3 * N1 + 2 * N2;
   c->tb.trace_src = c->trace_tabs;
   c->tb.trace_perm = c->trace_tabs + TRACE_STEPS * N2;
+  const auto ftw = fft1_twiddles();
+  if (hipMalloc(&c->fft1, ftw.size() * sizeof(double2)) != hipSuccess)
+    return fail(set_error(OMR_ERR_OUT_OF_MEMORY, "omr_ctx_create: tables"));
+  hipMemcpy(c->fft1, ftw.data(), ftw.size() * sizeof(double2), hipMemcpyHostToDevice);
+  c->tb.fft1 = c->fft1;
   // keys
-  if (hipMalloc(&c->bsk1, BSK1_ELEMS * sizeof(Key1T)) != hipSuccess ||
+  const bool fft1 = OMR_FFT1 != 0;
+  if ((fft1 ? hipMalloc(&c->bsk1f, BSK1_ELEMS / 2 * sizeof(double2))
+            : hipMalloc(&c->bsk1, BSK1_ELEMS * sizeof(Key1T))) != hipSuccess ||
       hipMalloc(&c->bsk2, BSK2_ELEMS * sizeof(double)) != hipSuccess ||
       hipMalloc(&c->tk, TK_ELEMS * sizeof(double)) != hipSuccess ||
       hipMalloc(&c->ksk, (KSK_ELEMS + 64) * sizeof(uint32_t)) != hipSuccess)
@@ -215,8 +274,9 @@ extern "C" omr_status omr_ctx_create(const omr_detection_key_view *key, int devi
   const double ninv1 = centred(h_powmod(N1, Q1 - 2, Q1), Q1);
   const double ninv2 = centred(h_powmod(N2, Q2 - 2, Q2), Q2);
   omr_status st;
-  if ((st = convert_keys<1, uint32_t, Key1T>(key->bsk1, BSK1_ELEMS / N1, c->bsk1, ninv1, c->tb.tw1,
-                                      c->stream)) != OMR_OK)
+  if ((st = fft1 ? convert_keys_fft1(key->bsk1, BSK1_ELEMS / N1, c->bsk1f, c->fft1, c->stream)
+                 : convert_keys<1, uint32_t, Key1T>(key->bsk1, BSK1_ELEMS / N1, c->bsk1, ninv1,
+                                                    c->tb.tw1, c->stream)) != OMR_OK)
     return fail(st);
   if ((st = convert_keys<2, uint64_t, double>(key->bsk2, BSK2_ELEMS / N2, c->bsk2, ninv2, c->tb.tw2,
                                       c->stream)) != OMR_OK)
@@ -239,7 +299,7 @@ extern "C" void omr_ctx_destroy(omr_ctx *c) {
   if (!c) return;
   hipSetDevice(c->device);
   if (c->stream) hipStreamSynchronize(c->stream);
-  for (void *p : {(void *)c->bsk1, (void *)c->bsk2, (void *)c->tk, (void *)c->ksk,
+  for (void *p : {(void *)c->bsk1, (void *)c->bsk1f, (void *)c->fft1, (void *)c->bsk2, (void *)c->tk, (void *)c->ksk,
                   (void *)c->tables, (void *)c->trace_tabs, (void *)c->ext, (void *)c->lwe1t,
                   (void *)c->lwe_int, (void *)c->s_clue_a, (void *)c->s_clue_b, (void *)c->s_out,
                   (void *)c->partial})
@@ -283,9 +343,9 @@ omr_status detect_device(omr_ctx *c, const uint16_t *ca, const uint16_t *cb, siz
     const int B = (int)std::min(c->batch, D - off);
     hipEvent_t *ev = c->timing ? &c->events[ch * 5] : nullptr;
     if (ev) HIP_TRY(hipEventRecord(ev[0], st));
-    br1_kernel<<<(unsigned)(B * CLUES), BR1_T, 0, st>>>(ca + off * N0, cb + off * CLUES, nullptr,
-                                                          nullptr, c->bsk1, c->tb, c->ext, nullptr, 0);
-    HIP_TRY(hipGetLastError());
+    if ((s = launch_br1(c, (size_t)B * CLUES, ca + off * N0, cb + off * CLUES, nullptr, nullptr,
+                        c->ext, nullptr, 0, st)) != OMR_OK)
+      return s;
     if (ev) HIP_TRY(hipEventRecord(ev[1], st));
     const size_t n7 = (size_t)B * (N1 + 1);
     sum7_kernel<<<(unsigned)((n7 + 255) / 256), 256, 0, st>>>(c->ext, c->lwe1t, B);
@@ -496,8 +556,9 @@ extern "C" omr_status omr_first_level(omr_ctx *c, const uint16_t *ca, const uint
   HIP_TRY(hipMemcpyAsync(c->s_clue_a, ca, D * N0 * sizeof(uint16_t), hipMemcpyHostToDevice, st));
   HIP_TRY(hipMemcpyAsync(c->s_clue_b, cb, D * CLUES * sizeof(uint16_t), hipMemcpyHostToDevice, st));
   const int B = (int)D;
-  br1_kernel<<<(unsigned)(B * CLUES), BR1_T, 0, st>>>(c->s_clue_a, c->s_clue_b, nullptr, nullptr,
-                                                        c->bsk1, c->tb, c->ext, nullptr, 0);
+  if ((s = launch_br1(c, (size_t)B * CLUES, c->s_clue_a, c->s_clue_b, nullptr, nullptr, c->ext,
+                      nullptr, 0, st)) != OMR_OK)
+    return s;
   const size_t n7 = (size_t)B * (N1 + 1);
   sum7_kernel<<<(unsigned)((n7 + 255) / 256), 256, 0, st>>>(c->ext, c->lwe1t, B);
   ks_kernel<KS_CT><<<dim3((B + 63) / 64, (NI + 1 + KS_CT - 1) / KS_CT), 64, 0, st>>>(c->lwe1t, c->ksk, c->lwe_int, B);
@@ -507,8 +568,36 @@ extern "C" omr_status omr_first_level(omr_ctx *c, const uint16_t *ca, const uint
   return OMR_OK;
 }
 
+extern "C" omr_status omr_fft1_mul(omr_ctx *c, const uint32_t *a, const uint32_t *k, size_t n,
+                                   uint64_t *out) {
+  if (!c || !a || !k || !out || n == 0)
+    return set_error(OMR_ERR_INVALID_ARGUMENT, "omr_fft1_mul: bad argument");
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  DevBuf<uint32_t> da, dk;
+  DevBuf<uint64_t> dout;
+  HIP_TRY(da.alloc(n * N1));
+  HIP_TRY(dk.alloc(n * N1));
+  HIP_TRY(dout.alloc(n * N1));
+  HIP_TRY(hipMemcpy(da.p, a, n * N1 * sizeof(uint32_t), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(dk.p, k, n * N1 * sizeof(uint32_t), hipMemcpyHostToDevice));
+  fft1_mul_kernel<<<(unsigned)n, 64, 0, c->stream>>>(da.p, dk.p, dout.p, c->fft1);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  HIP_TRY(hipMemcpy(out, dout.p, n * N1 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  return OMR_OK;
+}
+
+extern "C" omr_status omr_blind_rotate_level1_mode(omr_ctx *c, const uint16_t *la,
+                                                   const uint16_t *lb, size_t n, uint64_t *out,
+                                                   int mode);
 extern "C" omr_status omr_blind_rotate_level1(omr_ctx *c, const uint16_t *la, const uint16_t *lb,
                                               size_t n, uint64_t *out) {
+  return omr_blind_rotate_level1_mode(c, la, lb, n, out, 1);
+}
+extern "C" omr_status omr_blind_rotate_level1_mode(omr_ctx *c, const uint16_t *la,
+                                                   const uint16_t *lb, size_t n, uint64_t *out,
+                                                   int mode) {
   if (!c || !la || !lb || !out || n == 0)
     return set_error(OMR_ERR_INVALID_ARGUMENT, "omr_blind_rotate_level1: bad argument");
   std::lock_guard<std::mutex> lk(c->mu);
@@ -520,9 +609,8 @@ extern "C" omr_status omr_blind_rotate_level1(omr_ctx *c, const uint16_t *la, co
   HIP_TRY(dout.alloc(n * 2 * N1));
   HIP_TRY(hipMemcpy(da.p, la, n * N0 * sizeof(uint16_t), hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(db.p, lb, n * sizeof(uint16_t), hipMemcpyHostToDevice));
-  br1_kernel<<<(unsigned)n, BR1_T, 0, c->stream>>>(nullptr, nullptr, da.p, db.p, c->bsk1, c->tb,
-                                                   nullptr, dout.p, 1);
-  HIP_TRY(hipGetLastError());
+  omr_status s = launch_br1(c, n, nullptr, nullptr, da.p, db.p, nullptr, dout.p, mode, c->stream);
+  if (s != OMR_OK) return s;
   HIP_TRY(hipStreamSynchronize(c->stream));
   HIP_TRY(hipMemcpy(out, dout.p, n * 2 * N1 * sizeof(uint64_t), hipMemcpyDeviceToHost));
   return OMR_OK;

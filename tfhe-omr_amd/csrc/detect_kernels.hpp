@@ -82,6 +82,12 @@ __device__ __forceinline__ double rot_read(const double *p, int j, int r) {
   return s * p[t];
 }
 
+}  // namespace omr
+
+#include "br1_fft.hpp"
+
+namespace omr {
+
 // ------------------------------------------------------------------------------------------
 // One CMUX step of the binary blind rotation (BlindRotationKey::blind_rotate):
 //   ACC += ((X^a - 1) * ACC) [x] GGSW_i

@@ -36,6 +36,9 @@ namespace omr {
 #ifndef OMR_PAIR2
 #define OMR_PAIR2 0       // level 2: paired mask/body digit transforms
 #endif
+#ifndef OMR_FFT1
+#define OMR_FFT1 1        // level 1: FP64 complex-FFT external product (br1_fft.hpp)
+#endif
 #ifndef OMR_KEY_NT
 #define OMR_KEY_NT 0
 #endif
@@ -62,6 +65,7 @@ struct DeviceTables {
   const double *lut1, *lut2;              // LUTs, coefficient domain (centred)
   const uint16_t *trace_perm;             // [11][2048] NTT-domain permutation of sigma_g
   const uint16_t *trace_src;              // [11][2048] coefficient source index of sigma_g (+N: negate)
+  const double2 *fft1;                    // level-1 FFT twiddles (device_fft.hpp)
 };
 
 // ---- key conversion: coefficient-domain canonical residues -> NTT-domain centred residues ----

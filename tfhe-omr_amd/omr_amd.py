@@ -78,6 +78,7 @@ EXPORTS = {
                                              C.c_void_p]),
     "omr_first_level": (C.c_int, [C.c_void_p, _u16p, _u16p, C.c_size_t, _u32p]),
     "omr_blind_rotate_level1": (C.c_int, [C.c_void_p, _u16p, _u16p, C.c_size_t, _u64p]),
+    "omr_fft1_mul": (C.c_int, [C.c_void_p, _u32p, _u32p, C.c_size_t, _u64p]),
     "omr_second_level": (C.c_int, [C.c_void_p, _u32p, C.c_size_t, _u64p]),
     "omr_blind_rotate_level2": (C.c_int, [C.c_void_p, _u32p, C.c_size_t, _u64p]),
     "omr_ntt": (C.c_int, [C.c_int, C.c_int, _u64p, C.c_size_t, C.c_int]),
@@ -295,6 +296,15 @@ class Detector:
         out = np.empty((lwe_a.shape[0], 2, N1), np.uint64)
         _check(lib().omr_blind_rotate_level1(self._h, lwe_a.reshape(-1), lwe_b, lwe_a.shape[0], out.reshape(-1)),
                "omr_blind_rotate_level1")
+        return out
+
+    def fft1_mul(self, a, k) -> np.ndarray:
+        """a * k mod (X^1024 + 1, q1) through the level-1 FFT path (a digit-sized)."""
+        a = np.ascontiguousarray(a, dtype=np.uint32).reshape(-1, N1)
+        k = np.ascontiguousarray(k, dtype=np.uint32).reshape(-1, N1)
+        out = np.empty(a.shape, np.uint64)
+        _check(lib().omr_fft1_mul(self._h, a.reshape(-1), k.reshape(-1), a.shape[0], out.reshape(-1)),
+               "omr_fft1_mul")
         return out
 
     def second_level(self, lwe_int) -> np.ndarray:
