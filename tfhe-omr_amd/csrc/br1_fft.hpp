@@ -18,7 +18,10 @@
 namespace omr {
 
 #ifndef BR1F_WAVES
-#define BR1F_WAVES 2  // waves per SIMD the register allocation targets (256 VGPRs)
+#define BR1F_WAVES (BR1F_RW > 1 ? 1 : 2)  // waves per SIMD the register allocation targets
+#endif
+#ifndef BR1F_RW
+#define BR1F_RW 1  // level-1 rotations per wave (key rows shared, transforms interleaved)
 #endif
 #ifndef BR1F_KEY_SPLIT
 #define BR1F_KEY_SPLIT 1  // load the B component of a key row after the transform (32 VGPRs less)
@@ -63,10 +66,9 @@ struct Lvl1Int {
 // ACC layout: ac[p][h * 8 + e] = coefficient lane + 64 e + 512 h of poly p (0 mask, 1 body).
 __device__ __forceinline__ int acc_coef(int lane, int i) { return lane + 64 * (i & 7) + 512 * (i >> 3); }
 
-// digits of (X^a - 1) * ACC for both polys (ACC staged through LDS)
-__device__ __forceinline__ void br1f_digits(const int (&ac)[2][16], double2 *xch, int a, int lane,
+// digits of (X^a - 1) * ACC for both polys (ACC staged through the LDS buffer st, 8 KB)
+__device__ __forceinline__ void br1f_digits(const int (&ac)[2][16], int *st, int a, int lane,
                                             uint32_t (&pk)[2][16]) {
-  int *st = reinterpret_cast<int *>(xch);  // [2][N1] int32 staging (8 KB)
 #pragma unroll
   for (int p = 0; p < 2; ++p)
 #pragma unroll
@@ -81,18 +83,27 @@ __device__ __forceinline__ void br1f_digits(const int (&ac)[2][16], double2 *xch
   __syncthreads();
 }
 
-__device__ __forceinline__ void br1f_step(int (&ac)[2][16], double2 *xch, const double2 *tws, int a,
-                                          const double2 *__restrict__ ggsw, int lane) {
+// One CMUX step for RW rotations held by this wave (all at the same key row i; a[r] may be 0,
+// which yields zero digits and leaves that accumulator unchanged). The key row loads are shared
+// by the RW rotations and the RW transforms are interleaved (instruction-level parallelism).
+template <int RW>
+__device__ __forceinline__ void br1f_step(int (&ac)[RW][2][16], double2 *xch, const double2 *tws,
+                                          const int (&a)[RW], const double2 *__restrict__ ggsw,
+                                          int lane) {
   using F = Fft512;
   constexpr int NF = F::N;
-  uint32_t pk[2][16];
-  br1f_digits(ac, xch, a, lane, pk);
+  uint32_t pk[RW][2][16];
+#pragma unroll
+  for (int r = 0; r < RW; ++r)
+    br1f_digits(ac[r], reinterpret_cast<int *>(xch + r * NF), a[r], lane, pk[r]);
 
-  double outr[2][8], outi[2][8];
+  double outr[2][RW][8], outi[2][RW][8];  // [output A/B][rotation][point]
 #pragma unroll
   for (int o = 0; o < 2; ++o)
 #pragma unroll
-    for (int e = 0; e < 8; ++e) outr[o][e] = outi[o][e] = 0.0;
+    for (int r = 0; r < RW; ++r)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) outr[o][r][e] = outi[o][r][e] = 0.0;
 #pragma unroll
   for (int p = 0; p < 2; ++p) {
 #pragma unroll 1
@@ -105,106 +116,124 @@ __device__ __forceinline__ void br1f_step(int (&ac)[2][16], double2 *xch, const 
         ka[e] = kr[e];
         if (!BR1F_KEY_SPLIT) kb[e] = kr[NF + e];
       }
-      double xr[8], xi[8];
+      double xr[RW][8], xi[RW][8];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        xr[e] = Lvl1Int::digit(pk[p][e], k);
-        xi[e] = Lvl1Int::digit(pk[p][8 + e], k);
-      }
-      F::fwd(xr, xi, xch, tws, lane);
+      for (int r = 0; r < RW; ++r)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          xr[r][e] = Lvl1Int::digit(pk[r][p][e], k);
+          xi[r][e] = Lvl1Int::digit(pk[r][p][8 + e], k);
+        }
+      F::fwd<RW>(xr, xi, xch, tws, lane);
       if (BR1F_KEY_SPLIT) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) kb[e] = kr[NF + e];
       }
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        outr[0][e] = __fma_rn(xr[e], ka[e].x, __fma_rn(-xi[e], ka[e].y, outr[0][e]));
-        outi[0][e] = __fma_rn(xr[e], ka[e].y, __fma_rn(xi[e], ka[e].x, outi[0][e]));
-        outr[1][e] = __fma_rn(xr[e], kb[e].x, __fma_rn(-xi[e], kb[e].y, outr[1][e]));
-        outi[1][e] = __fma_rn(xr[e], kb[e].y, __fma_rn(xi[e], kb[e].x, outi[1][e]));
-      }
+      for (int r = 0; r < RW; ++r)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          outr[0][r][e] = __fma_rn(xr[r][e], ka[e].x, __fma_rn(-xi[r][e], ka[e].y, outr[0][r][e]));
+          outi[0][r][e] = __fma_rn(xr[r][e], ka[e].y, __fma_rn(xi[r][e], ka[e].x, outi[0][r][e]));
+          outr[1][r][e] = __fma_rn(xr[r][e], kb[e].x, __fma_rn(-xi[r][e], kb[e].y, outr[1][r][e]));
+          outi[1][r][e] = __fma_rn(xr[r][e], kb[e].y, __fma_rn(xi[r][e], kb[e].x, outi[1][r][e]));
+        }
     }
   }
 #pragma unroll
   for (int o = 0; o < 2; ++o) {
-    F::inv(outr[o], outi[o], xch, tws, lane);
+    F::inv<RW>(outr[o], outi[o], xch, tws, lane);
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const double v = rint(i < 8 ? outr[o][i] : outi[o][i - 8]);  // exact integer (< 2^43)
-      ac[o][i] = Lvl1Int::canon(ac[o][i] + (int)red<Mod<1>>(v));
-    }
+    for (int r = 0; r < RW; ++r)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const double v = rint(i < 8 ? outr[o][r][i] : outi[o][r][i - 8]);  // exact (< 2^43)
+        ac[r][o][i] = Lvl1Int::canon(ac[r][o][i] + (int)red<Mod<1>>(v));
+      }
   }
 }
 
+// Level-1 blind rotations, RW per wave (one wave per workgroup); rotation g = wg * RW + r:
+// input either clue g % 7 of message g / 7 (lwe_a == nullptr) or LWE g. nrot bounds g.
+template <int RW>
 __global__ __launch_bounds__(64, BR1F_WAVES) void br1f_kernel(const uint16_t *__restrict__ clue_a,
                                                       const uint16_t *__restrict__ clue_b,
                                                       const uint16_t *__restrict__ lwe_a,
                                                       const uint16_t *__restrict__ lwe_b,
                                                       const double2 *__restrict__ bskf, DeviceTables tb,
                                                       uint32_t *__restrict__ ext,
-                                                      uint64_t *__restrict__ rlwe_out, int mode) {
+                                                      uint64_t *__restrict__ rlwe_out, int mode,
+                                                      size_t nrot) {
   constexpr int NF = Fft512::N;
-  __shared__ double2 xch[NF];
+  __shared__ double2 xch[RW * NF];
   __shared__ double2 tws[NF];
-  __shared__ uint16_t la[N0];
+  __shared__ uint16_t la[RW][N0];
   const int lane = threadIdx.x;
-  const size_t wg = blockIdx.x;
-  int b;
-  if (lwe_a == nullptr) {  // extract clue c of message m (CmLweCiphertext::extract_all, :514)
-    const size_t m = wg / CLUES;
-    const int c = (int)(wg % CLUES);
-    const uint16_t *A = clue_a + m * N0;
-    for (int i = lane; i < N0; i += 64)
-      la[i] = i <= c ? (uint16_t)(A[c - i] & (Q0 - 1)) : (uint16_t)((Q0 - A[N0 + c - i]) & (Q0 - 1));
-    b = clue_b[m * CLUES + c] & (Q0 - 1);
-  } else {
-    for (int i = lane; i < N0; i += 64) la[i] = lwe_a[wg * N0 + i] & (Q0 - 1);
-    b = lwe_b[wg] & (Q0 - 1);
+  int b[RW];
+  size_t g[RW];
+#pragma unroll
+  for (int r = 0; r < RW; ++r) {
+    g[r] = (size_t)blockIdx.x * RW + r;
+    const size_t gi = g[r] < nrot ? g[r] : nrot - 1;  // a tail slot recomputes the last rotation
+    if (lwe_a == nullptr) {  // extract clue c of message m (CmLweCiphertext::extract_all, :514)
+      const size_t m = gi / CLUES;
+      const int c = (int)(gi % CLUES);
+      const uint16_t *A = clue_a + m * N0;
+      for (int i = lane; i < N0; i += 64)
+        la[r][i] = i <= c ? (uint16_t)(A[c - i] & (Q0 - 1)) : (uint16_t)((Q0 - A[N0 + c - i]) & (Q0 - 1));
+      b[r] = clue_b[m * CLUES + c] & (Q0 - 1);
+    } else {
+      for (int i = lane; i < N0; i += 64) la[r][i] = lwe_a[gi * N0 + i] & (Q0 - 1);
+      b[r] = lwe_b[gi] & (Q0 - 1);
+    }
   }
   // ACC = (0, X^{-b} * LUT1)
-  int ac[2][16];
-  const int r0 = (2 * N1 - (b % (2 * N1))) % (2 * N1);
+  int ac[RW][2][16];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    ac[0][i] = 0;
-    ac[1][i] = (int)canon_small<Mod<1>>(rot_read<N1>(tb.lut1, acc_coef(lane, i), r0));
+  for (int r = 0; r < RW; ++r) {
+    const int r0 = (2 * N1 - (b[r] % (2 * N1))) % (2 * N1);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      ac[r][0][i] = 0;
+      ac[r][1][i] = (int)canon_small<Mod<1>>(rot_read<N1>(tb.lut1, acc_coef(lane, i), r0));
+    }
   }
 #pragma unroll
   for (int e = 0; e < 8; ++e) tws[lane + 64 * e] = tb.fft1[lane + 64 * e];
   __syncthreads();
 #pragma unroll 1
   for (int i = 0; i < N0; ++i) {
-    const int a = __builtin_amdgcn_readfirstlane(la[i]);
-    if (a == 0) continue;  // (X^0 - 1) * ACC = 0
-    if (mode == 2) {  // debug: packed digits of the first CMUX step
-      uint32_t pk[2][16];
-      br1f_digits(ac, xch, a, lane, pk);
+    int a[RW], any = 0;
 #pragma unroll
-      for (int p = 0; p < 2; ++p)
-#pragma unroll
-        for (int j = 0; j < 16; ++j) rlwe_out[wg * 2 * N1 + p * N1 + acc_coef(lane, j)] = pk[p][j];
-      return;
+    for (int r = 0; r < RW; ++r) {
+      a[r] = __builtin_amdgcn_readfirstlane(la[r][i]);
+      any |= a[r];
     }
-    br1f_step(ac, xch, tws, a, bskf + (size_t)i * (2 * D1 * 2 * NF), lane);
+    if (any == 0) continue;  // (X^0 - 1) * ACC = 0
+    br1f_step<RW>(ac, xch, tws, a, bskf + (size_t)i * (2 * D1 * 2 * NF), lane);
   }
-  if (mode == 0) {  // extract_lwe_locally (coefficient 0), detector.rs:561
-    int *st = reinterpret_cast<int *>(xch);
 #pragma unroll
-    for (int i = 0; i < 16; ++i) st[acc_coef(lane, i)] = ac[0][i];
-    __syncthreads();
-    uint32_t *o = ext + wg * (N1 + 1);
+  for (int r = 0; r < RW; ++r) {
+    if (g[r] >= nrot) break;
+    if (mode == 0) {  // extract_lwe_locally (coefficient 0), detector.rs:561
+      int *st = reinterpret_cast<int *>(xch + r * NF);
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int j = acc_coef(lane, i);
-      o[j] = Lvl1Int::to_u32(j == 0 ? st[0] : -st[N1 - j]);
-    }
-    if (lane == 0) o[N1] = Lvl1Int::to_u32(ac[1][0]);
-  } else {
-    uint64_t *o = rlwe_out + wg * 2 * N1;
+      for (int i = 0; i < 16; ++i) st[acc_coef(lane, i)] = ac[r][0][i];
+      __syncthreads();
+      uint32_t *o = ext + g[r] * (N1 + 1);
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      o[acc_coef(lane, i)] = Lvl1Int::to_u32(ac[0][i]);
-      o[N1 + acc_coef(lane, i)] = Lvl1Int::to_u32(ac[1][i]);
+      for (int i = 0; i < 16; ++i) {
+        const int j = acc_coef(lane, i);
+        o[j] = Lvl1Int::to_u32(j == 0 ? st[0] : -st[N1 - j]);
+      }
+      if (lane == 0) o[N1] = Lvl1Int::to_u32(ac[r][1][0]);
+    } else if (mode == 1) {
+      uint64_t *o = rlwe_out + g[r] * 2 * N1;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        o[acc_coef(lane, i)] = Lvl1Int::to_u32(ac[r][0][i]);
+        o[N1 + acc_coef(lane, i)] = Lvl1Int::to_u32(ac[r][1][i]);
+      }
     }
   }
 }

@@ -69,18 +69,20 @@ std::vector<double> negacyclic_lut(const std::vector<uint64_t> &v, int N, int lo
   return lut;
 }
 
-// Level-1 FFT twiddles (device_fft.hpp): tw[(1 << s) + i] = w^(eps(s, i) / 2), w = exp(i pi / 1024),
+// Level-1 FFT twiddles (device_fft.hpp): node i of stage s -> w^(eps(s, i) / 2), w = exp(i pi / 1024),
 // eps(0, 0) = 512, eps(s+1, 2i) = eps(s, i) / 2, eps(s+1, 2i+1) = eps(s, i) / 2 + 1024 (mod 2048).
-// Evaluated in long double and rounded once.
+// Evaluated in long double and rounded once; stages 6-8 stored lane-minor (Fft512::twiddle_index).
 std::vector<double2> fft1_twiddles() {
   std::vector<double2> tw(512, make_double2(1.0, 0.0));
   std::vector<int> eps{512};
   for (int s = 0; s < 9; ++s) {
     std::vector<int> next;
+    const int k = s - 6;  // stage within the last pass
     for (int i = 0; i < (1 << s); ++i) {
       const int half = eps[i] / 2;
       const long double ang = 3.14159265358979323846264338327950288L * (long double)half / 1024.0L;
-      tw[(1 << s) + i] = make_double2((double)cosl(ang), (double)sinl(ang));
+      const int pos = k < 0 ? (1 << s) + i : (1 << s) + (i & ((1 << k) - 1)) * 64 + (i >> k);
+      tw[pos] = make_double2((double)cosl(ang), (double)sinl(ang));
       next.push_back(half % 2048);
       next.push_back((half + 1024) % 2048);
     }
@@ -185,7 +187,8 @@ omr_status launch_br1(omr_ctx *c, size_t n, const uint16_t *ca, const uint16_t *
                       const uint16_t *la, const uint16_t *lb, uint32_t *ext, uint64_t *rlwe, int mode,
                       hipStream_t st) {
 #if OMR_FFT1
-  br1f_kernel<<<(unsigned)n, 64, 0, st>>>(ca, cb, la, lb, c->bsk1f, c->tb, ext, rlwe, mode);
+  br1f_kernel<BR1F_RW><<<(unsigned)((n + BR1F_RW - 1) / BR1F_RW), 64, 0, st>>>(
+      ca, cb, la, lb, c->bsk1f, c->tb, ext, rlwe, mode, n);
 #else
   br1_kernel<<<(unsigned)n, BR1_T, 0, st>>>(ca, cb, la, lb, c->bsk1, c->tb, ext, rlwe, mode);
 #endif
@@ -588,16 +591,8 @@ extern "C" omr_status omr_fft1_mul(omr_ctx *c, const uint32_t *a, const uint32_t
   return OMR_OK;
 }
 
-extern "C" omr_status omr_blind_rotate_level1_mode(omr_ctx *c, const uint16_t *la,
-                                                   const uint16_t *lb, size_t n, uint64_t *out,
-                                                   int mode);
 extern "C" omr_status omr_blind_rotate_level1(omr_ctx *c, const uint16_t *la, const uint16_t *lb,
                                               size_t n, uint64_t *out) {
-  return omr_blind_rotate_level1_mode(c, la, lb, n, out, 1);
-}
-extern "C" omr_status omr_blind_rotate_level1_mode(omr_ctx *c, const uint16_t *la,
-                                                   const uint16_t *lb, size_t n, uint64_t *out,
-                                                   int mode) {
   if (!c || !la || !lb || !out || n == 0)
     return set_error(OMR_ERR_INVALID_ARGUMENT, "omr_blind_rotate_level1: bad argument");
   std::lock_guard<std::mutex> lk(c->mu);
@@ -609,7 +604,7 @@ extern "C" omr_status omr_blind_rotate_level1_mode(omr_ctx *c, const uint16_t *l
   HIP_TRY(dout.alloc(n * 2 * N1));
   HIP_TRY(hipMemcpy(da.p, la, n * N0 * sizeof(uint16_t), hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(db.p, lb, n * sizeof(uint16_t), hipMemcpyHostToDevice));
-  omr_status s = launch_br1(c, n, nullptr, nullptr, da.p, db.p, nullptr, dout.p, mode, c->stream);
+  omr_status s = launch_br1(c, n, nullptr, nullptr, da.p, db.p, nullptr, dout.p, 1, c->stream);
   if (s != OMR_OK) return s;
   HIP_TRY(hipStreamSynchronize(c->stream));
   HIP_TRY(hipMemcpy(out, dout.p, n * 2 * N1 * sizeof(uint64_t), hipMemcpyDeviceToHost));
