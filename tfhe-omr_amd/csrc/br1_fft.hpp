@@ -210,7 +210,11 @@ __global__ __launch_bounds__(64, BR1F_WAVES) void br1f_kernel(const uint16_t *__
       any |= a[r];
     }
     if (any == 0) continue;  // (X^0 - 1) * ACC = 0
+#ifdef OMR_EXPT_KEYWRAP  // timing experiment only: every step reads one of 4 L2-resident key rows
+    br1f_step<RW>(ac, xch, tws, a, bskf + (size_t)(i & 3) * (2 * D1 * 2 * NF), lane);
+#else
     br1f_step<RW>(ac, xch, tws, a, bskf + (size_t)i * (2 * D1 * 2 * NF), lane);
+#endif
   }
 #pragma unroll
   for (int r = 0; r < RW; ++r) {

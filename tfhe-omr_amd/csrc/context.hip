@@ -69,22 +69,25 @@ std::vector<double> negacyclic_lut(const std::vector<uint64_t> &v, int N, int lo
   return lut;
 }
 
-// Level-1 FFT twiddles (device_fft.hpp): node i of stage s -> w^(eps(s, i) / 2), w = exp(i pi / 1024),
-// eps(0, 0) = 512, eps(s+1, 2i) = eps(s, i) / 2, eps(s+1, 2i+1) = eps(s, i) / 2 + 1024 (mod 2048).
-// Evaluated in long double and rounded once; stages 6-8 stored lane-minor (Fft512::twiddle_index).
-std::vector<double2> fft1_twiddles() {
-  std::vector<double2> tw(512, make_double2(1.0, 0.0));
-  std::vector<int> eps{512};
-  for (int s = 0; s < 9; ++s) {
+// FFT twiddles of WgFft<T, E, L> (device_fft.hpp): node i of stage s -> w^(eps(s, i) / 2),
+// w = exp(i pi / 2n), n = 2^L, eps(0, 0) = n, eps(s+1, 2i) = eps(s, i) / 2,
+// eps(s+1, 2i+1) = eps(s, i) / 2 + 2n (mod 4n). Evaluated in long double and rounded once;
+// the last pass's stages stored lane-minor (WgFft::twiddle_index).
+std::vector<double2> fft_twiddles(int T, int E, int L) {
+  const int n = 1 << L, R = __builtin_ctz(E);
+  std::vector<double2> tw(n, make_double2(1.0, 0.0));
+  std::vector<int> eps{n};
+  for (int s = 0; s < L; ++s) {
     std::vector<int> next;
-    const int k = s - 6;  // stage within the last pass
+    const int k = s - (L - R);  // stage within the last pass (< 0: earlier pass)
     for (int i = 0; i < (1 << s); ++i) {
       const int half = eps[i] / 2;
-      const long double ang = 3.14159265358979323846264338327950288L * (long double)half / 1024.0L;
-      const int pos = k < 0 ? (1 << s) + i : (1 << s) + (i & ((1 << k) - 1)) * 64 + (i >> k);
+      const long double ang =
+          3.14159265358979323846264338327950288L * (long double)half / (long double)(2 * n);
+      const int pos = k < 0 ? (1 << s) + i : (1 << s) + (i & ((1 << k) - 1)) * T + (i >> k);
       tw[pos] = make_double2((double)cosl(ang), (double)sinl(ang));
-      next.push_back(half % 2048);
-      next.push_back((half + 1024) % 2048);
+      next.push_back(half % (4 * n));
+      next.push_back((half + 2 * n) % (4 * n));
     }
     eps.swap(next);
   }
@@ -98,7 +101,8 @@ struct omr_ctx {
   hipStream_t stream = nullptr;
   Key1T *bsk1 = nullptr;    // level-1 NTT-domain keys (OMR_FFT1 == 0)
   double2 *bsk1f = nullptr; // level-1 FFT-domain keys (OMR_FFT1)
-  double2 *fft1 = nullptr;
+  double2 *fft1 = nullptr, *fft2 = nullptr;
+  double2 *bsk2f = nullptr; // level-2 FFT-domain key limbs (OMR_FFT2)
   double *bsk2 = nullptr, *tk = nullptr;
   uint32_t *ksk = nullptr;
   double *tables = nullptr;  // tw1 itw1 tw2 itw2 lut1 lut2
@@ -196,6 +200,34 @@ omr_status launch_br1(omr_ctx *c, size_t n, const uint16_t *ca, const uint16_t *
   return OMR_OK;
 }
 
+omr_status convert_keys_fft2(const uint64_t *host, size_t npoly, double2 *dev, const double2 *tw,
+                             hipStream_t st) {
+  const size_t chunk = 4096;
+  uint64_t *tmp = nullptr;
+  HIP_TRY(hipMalloc(&tmp, chunk * N2 * sizeof(uint64_t)));
+  for (size_t p0 = 0; p0 < npoly; p0 += chunk) {
+    const size_t n = std::min(chunk, npoly - p0);
+    HIP_TRY(hipMemcpyAsync(tmp, host + p0 * N2, n * N2 * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+    key_to_fft2_kernel<<<n, 256, 0, st>>>(tmp, dev + p0 * 2 * Fft1024::N, n, tw);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(st));
+  }
+  (void)hipFree(tmp);
+  return OMR_OK;
+}
+
+// Level-2 blind rotation (+ trace, mode 0) of n LWE(670, 4096) ciphertexts.
+omr_status launch_br2(omr_ctx *c, size_t n, const uint32_t *lwe_int, uint64_t *out, int mode,
+                      hipStream_t st) {
+#if OMR_FFT2
+  br2f_trace_kernel<<<(unsigned)n, BR2_T, 0, st>>>(lwe_int, c->bsk2f, c->tk, c->tb, out, mode);
+#else
+  br2_trace_kernel<<<(unsigned)n, BR2_T, 0, st>>>(lwe_int, c->bsk2, c->tk, c->tb, out, mode);
+#endif
+  HIP_TRY(hipGetLastError());
+  return OMR_OK;
+}
+
 }  // namespace
 
 // Scale the even (alpha) rows of the trace key by N^-1 in place.
@@ -261,16 +293,22 @@ extern "C" omr_status omr_ctx_create(const omr_detection_key_view *key, int devi
   c->tb.lut2 = c->tables + 3 * N1 + 2 * N2;
   c->tb.trace_src = c->trace_tabs;
   c->tb.trace_perm = c->trace_tabs + TRACE_STEPS * N2;
-  const auto ftw = fft1_twiddles();
+  const auto ftw = fft_twiddles(Fft512::T, Fft512::E, Fft512::L);
   if (hipMalloc(&c->fft1, ftw.size() * sizeof(double2)) != hipSuccess)
     return fail(set_error(OMR_ERR_OUT_OF_MEMORY, "omr_ctx_create: tables"));
   hipMemcpy(c->fft1, ftw.data(), ftw.size() * sizeof(double2), hipMemcpyHostToDevice);
   c->tb.fft1 = c->fft1;
+  const auto ftw2 = fft_twiddles(Fft1024::T, Fft1024::E, Fft1024::L);
+  if (hipMalloc(&c->fft2, ftw2.size() * sizeof(double2)) != hipSuccess)
+    return fail(set_error(OMR_ERR_OUT_OF_MEMORY, "omr_ctx_create: tables"));
+  hipMemcpy(c->fft2, ftw2.data(), ftw2.size() * sizeof(double2), hipMemcpyHostToDevice);
+  c->tb.fft2 = c->fft2;
   // keys
-  const bool fft1 = OMR_FFT1 != 0;
+  const bool fft1 = OMR_FFT1 != 0, fft2 = OMR_FFT2 != 0;
   if ((fft1 ? hipMalloc(&c->bsk1f, BSK1_ELEMS / 2 * sizeof(double2))
             : hipMalloc(&c->bsk1, BSK1_ELEMS * sizeof(Key1T))) != hipSuccess ||
-      hipMalloc(&c->bsk2, BSK2_ELEMS * sizeof(double)) != hipSuccess ||
+      (fft2 ? hipMalloc(&c->bsk2f, BSK2_ELEMS * sizeof(double2))
+            : hipMalloc(&c->bsk2, BSK2_ELEMS * sizeof(double))) != hipSuccess ||
       hipMalloc(&c->tk, TK_ELEMS * sizeof(double)) != hipSuccess ||
       hipMalloc(&c->ksk, (KSK_ELEMS + 64) * sizeof(uint32_t)) != hipSuccess)
     return fail(set_error(OMR_ERR_OUT_OF_MEMORY, "omr_ctx_create: key buffers"));
@@ -281,8 +319,9 @@ extern "C" omr_status omr_ctx_create(const omr_detection_key_view *key, int devi
                  : convert_keys<1, uint32_t, Key1T>(key->bsk1, BSK1_ELEMS / N1, c->bsk1, ninv1,
                                                     c->tb.tw1, c->stream)) != OMR_OK)
     return fail(st);
-  if ((st = convert_keys<2, uint64_t, double>(key->bsk2, BSK2_ELEMS / N2, c->bsk2, ninv2, c->tb.tw2,
-                                      c->stream)) != OMR_OK)
+  if ((st = fft2 ? convert_keys_fft2(key->bsk2, BSK2_ELEMS / N2, c->bsk2f, c->fft2, c->stream)
+                 : convert_keys<2, uint64_t, double>(key->bsk2, BSK2_ELEMS / N2, c->bsk2, ninv2,
+                                                     c->tb.tw2, c->stream)) != OMR_OK)
     return fail(st);
   if ((st = convert_keys<2, uint64_t, double>(key->trace_key, TK_ELEMS / N2, c->tk, 1.0, c->tb.tw2,
                                       c->stream)) != OMR_OK)
@@ -302,7 +341,7 @@ extern "C" void omr_ctx_destroy(omr_ctx *c) {
   if (!c) return;
   hipSetDevice(c->device);
   if (c->stream) hipStreamSynchronize(c->stream);
-  for (void *p : {(void *)c->bsk1, (void *)c->bsk1f, (void *)c->fft1, (void *)c->bsk2, (void *)c->tk, (void *)c->ksk,
+  for (void *p : {(void *)c->bsk1, (void *)c->bsk1f, (void *)c->fft1, (void *)c->fft2, (void *)c->bsk2f, (void *)c->bsk2, (void *)c->tk, (void *)c->ksk,
                   (void *)c->tables, (void *)c->trace_tabs, (void *)c->ext, (void *)c->lwe1t,
                   (void *)c->lwe_int, (void *)c->s_clue_a, (void *)c->s_clue_b, (void *)c->s_out,
                   (void *)c->partial})
@@ -355,9 +394,7 @@ omr_status detect_device(omr_ctx *c, const uint16_t *ca, const uint16_t *cb, siz
     ks_kernel<KS_CT><<<dim3((B + 63) / 64, (NI + 1 + KS_CT - 1) / KS_CT), 64, 0, st>>>(c->lwe1t, c->ksk, c->lwe_int, B);
     HIP_TRY(hipGetLastError());
     if (ev) HIP_TRY(hipEventRecord(ev[2], st));
-    br2_trace_kernel<<<(unsigned)B, BR2_T, 0, st>>>(c->lwe_int, c->bsk2, c->tk, c->tb,
-                                                    out + off * 2 * N2, 0);
-    HIP_TRY(hipGetLastError());
+    if ((s = launch_br2(c, (size_t)B, c->lwe_int, out + off * 2 * N2, 0, st)) != OMR_OK) return s;
     if (ev) HIP_TRY(hipEventRecord(ev[3], st));
   }
   return OMR_OK;
@@ -622,7 +659,8 @@ static omr_status second_level_impl(omr_ctx *c, const uint32_t *lwe, size_t n, u
   HIP_TRY(dl.alloc(n * (NI + 1)));
   HIP_TRY(dout.alloc(n * 2 * N2));
   HIP_TRY(hipMemcpy(dl.p, lwe, n * (NI + 1) * sizeof(uint32_t), hipMemcpyHostToDevice));
-  br2_trace_kernel<<<(unsigned)n, BR2_T, 0, c->stream>>>(dl.p, c->bsk2, c->tk, c->tb, dout.p, mode);
+  omr_status ls = launch_br2(c, n, dl.p, dout.p, mode, c->stream);
+  if (ls != OMR_OK) return ls;
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(c->stream));
   HIP_TRY(hipMemcpy(out, dout.p, n * 2 * N2 * sizeof(uint64_t), hipMemcpyDeviceToHost));

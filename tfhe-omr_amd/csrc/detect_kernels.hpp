@@ -306,7 +306,7 @@ __global__ __launch_bounds__(BR1_T, BR1_WAVES) void br1_kernel(const uint16_t *_
                                                    uint64_t *__restrict__ rlwe_out, int mode) {
   using M = Mod<1>;
   constexpr int T = BR1_T, E = BR1_E, N = N1;
-  __shared__ double xch[OMR_PAIR1 ? 2 * N : N];
+  __shared__ double xch[(OMR_PAIR1 ? 2 : 1) * WgNtt<M, T, E>::LDS_DOUBLES];
   __shared__ double tws[2 * N];
   __shared__ uint16_t la[N0];
   const int tid = threadIdx.x;
@@ -420,48 +420,16 @@ __global__ __launch_bounds__(64) void ks_kernel(const uint32_t *__restrict__ lwe
 }
 constexpr int KS_CT = 16;
 
-// ------------------------------------------------------------------------------------------
-// Level 2 (second_level_bootstrapping, detector.rs:599-624) fused with hom_trace (:626-639):
-// one workgroup per message. mode 0: trace + NTT output u64 [wg][2][N2] (NttRlweCiphertext);
-// mode 1: blind rotation only, coefficient-domain output (stage test).
-// ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(BR2_T, BR2_WAVES) void br2_trace_kernel(const uint32_t *__restrict__ lwe_int,
-                                                         const Key2T *__restrict__ bsk2,
-                                                         const double *__restrict__ tk,
-                                                         DeviceTables tb,
-                                                         uint64_t *__restrict__ out, int mode) {
+// hom_trace (detector.rs:626-639) of the level-2 accumulator (coefficient layout tid + e*T,
+// canonical) and store of NTT(c) as NttRlweCiphertext u64 [2][N2] at o. tw/itw: NTT twiddles in
+// LDS; xch: N2 doubles of LDS.
+__device__ __forceinline__ void hom_trace_store(double (&acc0)[BR2_E], double (&acc1)[BR2_E],
+                                                double *xch, const double *tw, const double *itw,
+                                                const double *__restrict__ tk, const DeviceTables &tb,
+                                                uint64_t *__restrict__ o, int tid) {
   using M = Mod<2>;
   constexpr int T = BR2_T, E = BR2_E, N = N2;
   using NTT = WgNtt<M, T, E>;
-  __shared__ double xch[OMR_PAIR2 ? 2 * N : N];
-  __shared__ double tws[2 * N];
-  const int tid = threadIdx.x;
-  const size_t wg = blockIdx.x;
-  const uint32_t *lwe = lwe_int + wg * (NI + 1);
-  double acc0[E], acc1[E];
-  br_init<2, T, E>(acc0, acc1, tb.lut2, (int)lwe[NI], tws, tb.tw2, tb.itw2, tid);
-  const double *tw = tws, *itw = tws + N;
-#pragma unroll 1
-  for (int i = 0; i < NI; ++i) {
-    const int a = (int)__builtin_amdgcn_readfirstlane(lwe[i]) & (2 * N - 1);
-    if (a == 0) continue;
-#if OMR_PAIR2
-    cmux_step_pair<2, T, E, LOGB2, D2, DROP2, Key2T, OMR_KEY_DEPTH2, false>(
-        acc0, acc1, xch, a, bsk2 + (size_t)i * (2 * D2 * 2 * N), tw, itw, tid);
-#else
-    cmux_step<2, T, E, LOGB2, D2, DROP2, Key2T, OMR_KEY_DEPTH2>(
-        acc0, acc1, xch, a, bsk2 + (size_t)i * (2 * D2 * 2 * N), tw, itw, tid);
-#endif
-  }
-  uint64_t *o = out + wg * 2 * N;
-  if (mode == 1) {
-#pragma unroll
-    for (int e = 0; e < E; ++e) {
-      o[tid + e * T] = to_u64<M>(acc0[e]);
-      o[N + tid + e * T] = to_u64<M>(acc1[e]);
-    }
-    return;
-  }
   // ---- hom_trace: c *= N^-1; for k: c += KS_k(sigma_g(c)); output NTT(c) ----
   // The mask stays in the coefficient domain (ca, layout tid + e*T); the body moves to the NTT
   // domain (cb, layout tid*E + e) where sigma_g is an index permutation.
@@ -543,4 +511,51 @@ __global__ __launch_bounds__(BR2_T, BR2_WAVES) void br2_trace_kernel(const uint3
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Level 2 (second_level_bootstrapping, detector.rs:599-624) fused with hom_trace (:626-639):
+// one workgroup per message. mode 0: trace + NTT output u64 [wg][2][N2] (NttRlweCiphertext);
+// mode 1: blind rotation only, coefficient-domain output (stage test).
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(BR2_T, BR2_WAVES) void br2_trace_kernel(const uint32_t *__restrict__ lwe_int,
+                                                         const Key2T *__restrict__ bsk2,
+                                                         const double *__restrict__ tk,
+                                                         DeviceTables tb,
+                                                         uint64_t *__restrict__ out, int mode) {
+  using M = Mod<2>;
+  constexpr int T = BR2_T, E = BR2_E, N = N2;
+  using NTT = WgNtt<M, T, E>;
+  __shared__ double xch[(OMR_PAIR2 ? 2 : 1) * NTT::LDS_DOUBLES];
+  __shared__ double tws[2 * N];
+  const int tid = threadIdx.x;
+  const size_t wg = blockIdx.x;
+  const uint32_t *lwe = lwe_int + wg * (NI + 1);
+  double acc0[E], acc1[E];
+  br_init<2, T, E>(acc0, acc1, tb.lut2, (int)lwe[NI], tws, tb.tw2, tb.itw2, tid);
+  const double *tw = tws, *itw = tws + N;
+#pragma unroll 1
+  for (int i = 0; i < NI; ++i) {
+    const int a = (int)__builtin_amdgcn_readfirstlane(lwe[i]) & (2 * N - 1);
+    if (a == 0) continue;
+#if OMR_PAIR2
+    cmux_step_pair<2, T, E, LOGB2, D2, DROP2, Key2T, OMR_KEY_DEPTH2, false>(
+        acc0, acc1, xch, a, bsk2 + (size_t)OMR_KEYROW2(i) * (2 * D2 * 2 * N), tw, itw, tid);
+#else
+    cmux_step<2, T, E, LOGB2, D2, DROP2, Key2T, OMR_KEY_DEPTH2>(
+        acc0, acc1, xch, a, bsk2 + (size_t)OMR_KEYROW2(i) * (2 * D2 * 2 * N), tw, itw, tid);
+#endif
+  }
+  uint64_t *o = out + wg * 2 * N;
+  if (mode == 1) {
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      o[tid + e * T] = to_u64<M>(acc0[e]);
+      o[N + tid + e * T] = to_u64<M>(acc1[e]);
+    }
+    return;
+  }
+  hom_trace_store(acc0, acc1, xch, tw, itw, tk, tb, o, tid);
+}
+
 }  // namespace omr
+
+#include "br2_fft.hpp"

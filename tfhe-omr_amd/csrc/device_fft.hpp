@@ -1,56 +1,74 @@
-// Wave-level 512-point complex FFT for the level-1 external product (gfx950).
+// Workgroup complex FFTs for the external products (gfx950).
 //
-// Level-1 residues are small: gadget digits satisfy |d| <= 17 and key coefficients |k| <= 2^26,
-// so every coefficient of sum_r d_r * k_r over the 8 GGSW rows is an integer below 2^43 and an
-// FP64 FFT product rounds to it exactly (worst error of a lane-exact model of this transform
-// with adversarial digits: 1.8e-3, tools/fft_exactness.py; rigorous FFT product bounds < 0.15). The transform
-// therefore replaces the 1024-point NTT mod q1 with a 512-point complex transform at ~45 % of
-// its FP64 work, and the results stay bit-identical to the modular computation.
+// Exactness: the external product only ever multiplies small gadget digits by key residues, so
+// every coefficient of sum_r digit_r * key_r is an integer well inside FP64's 53 bits and an FP64
+// FFT product rounds to it exactly:
+//   level 1: |d| <= 17, |k| <= 2^26, 8 rows, N = 1024: |coef| < 2^43; worst error of a lane-exact
+//            model with adversarial digits 1.8e-3 (tools/fft_exactness.py), rigorous bound < 0.15;
+//   level 2: |d| <= 64, keys split in two 25-bit limbs |k_l| <= 2^24, 12 rows, N = 2048:
+//            |coef| < 2^44.6; worst adversarial error 2e-3 (tools/fft_exactness.py --level 2).
+// Replacing the modular NTTs by half-length complex FFTs removes ~45 % (level 1) and ~40 %
+// (level 2) of the FP64 work, with bit-identical results.
 //
-// Ring map: R[X]/(X^1024 + 1) -> C[X]/(X^512 - i), p -> z with z_j = p_j + i p_{j+512}.
-// X^512 - i splits over the roots w^(1+4k) (w = exp(i pi / 1024)); the forward transform is a
+// Ring map: R[X]/(X^2n + 1) -> C[X]/(X^n - i), p -> z with z_j = p_j + i p_{j+n}, n = 2^L.
+// X^n - i splits over the roots w^(1+4k) (w = exp(i pi / 2n)); the forward transform is a
 // Cooley-Tukey tree on that factorisation (the twist is folded into the twiddles), the inverse a
-// Gentleman-Sande tree with conjugate twiddles, unscaled (the 1/512 is folded into the keys).
+// Gentleman-Sande tree with conjugate twiddles, unscaled (the 1/n is folded into the keys).
+// Node i of stage s uses w^(eps(s, i) / 2), eps(0, 0) = n, eps(s+1, 2i) = eps(s, i) / 2,
+// eps(s+1, 2i+1) = eps(s, i) / 2 + 2n (mod 4n); table layout in twiddle_index.
 //
-// One wave (64 lanes) owns a transform (or C interleaved ones), 8 complex values per lane, 3
-// radix-2 stages per pass, 2 LDS exchanges per transform (wave-private 8 KB buffer, XOR swizzle found by
-// tools/fft_lds_banks.py: no bank conflicts for ds_write_b128 / ds_read_b128).
-//   forward: in  x[e] = coefficient (lane + 64 e)    out x[e] = transform index (8 lane + e)
-//   inverse: in  x[e] = transform index (8 lane + e)  out x[e] = coefficient (lane + 64 e)
-// Twiddles: node i of stage s uses w^(eps(s, i) / 2) with eps(0, 0) = 512,
-// eps(s+1, 2i) = eps(s, i) / 2, eps(s+1, 2i+1) = eps(s, i) / 2 + 1024 (mod 2048); table layout in
-// twiddle_index (stages 0-5 at (1 << s) + i, stages 6-8 lane-minor).
+// T lanes hold E complex values each (N = T E), log2(E) radix-2 stages per pass, an LDS exchange
+// between passes (XOR swizzle found by tools/fft_lds_banks.py: no bank conflicts for
+// ds_write_b128 / ds_read_b128), C independent transforms interleaved.
+//   forward: in  x[e] = coefficient (lane + T e)    out x[e] = transform index (E lane + e)
+//   inverse: in  x[e] = transform index (E lane + e) out x[e] = coefficient (lane + T e)
 #pragma once
+
+#include <utility>
 
 #include "device_ntt.hpp"
 
 namespace omr {
 
-struct Fft512 {
-  static constexpr int T = 64, E = 8, N = 512, L = 9, R = 3, NPASS = 3;
+template <int T, int E, int L>
+struct FftSwizzle;
+template <>
+struct FftSwizzle<64, 8, 9> {  // tools/fft_lds_banks.py 64 8 9
+  static constexpr int M[6] = {4, 9, 15, 14, 0, 8};
+};
+template <>
+struct FftSwizzle<256, 4, 10> {  // tools/fft_lds_banks.py 256 4 10
+  static constexpr int M[7] = {2, 13, 6, 0, 4, 4, 2};
+};
 
-  // element index of register e in pass p (the WgNtt scheme with r == R in every pass)
+template <int T_, int E_, int L_>
+struct WgFft {
+  static constexpr int T = T_, E = E_, L = L_, N = T * E, R = ilog2(E), NPASS = L / R;
+  static_assert(N == (1 << L) && L % R == 0, "FFT geometry");
+
+  // element index of register e in pass p
   __device__ static __forceinline__ int index(int p, int lane, int e) {
     const int lb = L - (p + 1) * R;
     return ((lane >> lb) << (L - p * R)) | (e << lb) | (lane & ((1 << lb) - 1));
   }
-  // bank-conflict-free XOR swizzle (linear over GF(2), so swz(a ^ b) == swz(a) ^ swz(b))
-  __device__ static __forceinline__ int swz(int j) {
-    return j ^ (((j >> 3) & 1) * 4) ^ (((j >> 4) & 1) * 9) ^ (((j >> 5) & 1) * 15) ^
-           (((j >> 6) & 1) * 14) ^ (((j >> 8) & 1) * 8);
+  // bank-conflict-free XOR swizzle (linear over GF(2); folds to constants per unrolled e)
+  template <int... B>
+  __device__ static __forceinline__ int swz_bits(int j, std::integer_sequence<int, B...>) {
+    return (0 ^ ... ^ (((j >> (3 + B)) & 1) * FftSwizzle<T, E, L>::M[B]));
   }
-
-  // Node twiddle of stage P*R + k for register e. The last pass's stages (6, 7, 8) are stored
-  // lane-minor (entry (1 << s) + j * 64 + lane holds node (lane << k) + j) so that a wave's
-  // ds_read_b128 hits 64 consecutive entries (no bank conflicts); earlier passes broadcast.
+  __device__ static __forceinline__ int swz(int j) {
+    return j ^ swz_bits(j, std::make_integer_sequence<int, L - 3>{});
+  }
+  // Node twiddle of stage P*R + k for register e. The last pass's stages are stored lane-minor
+  // (entry (1 << s) + j * T + lane holds node (lane << k) + j) so a wave reads consecutive
+  // entries; in earlier passes lanes of a group share (broadcast) entries.
   template <int P>
   __device__ static __forceinline__ int twiddle_index(int k, int e, int lane) {
     constexpr int s0 = P * R, lb = L - s0 - R;
-    if constexpr (P == NPASS - 1) return (1 << (s0 + k)) + ((e >> (R - k)) << 6) + lane;
+    if constexpr (P == NPASS - 1) return (1 << (s0 + k)) + (e >> (R - k)) * T + lane;
     return (1 << (s0 + k)) + (((lane >> lb) << k) | (e >> (R - k)));
   }
 
-  // C independent transforms interleaved (C x 8 complex per lane, C LDS buffers of 512)
   template <int C>
   __device__ static __forceinline__ void exchange(double (&xr)[C][E], double (&xi)[C][E],
                                                   double2 *lds, int lane, int p_from, int p_to) {
@@ -74,7 +92,6 @@ struct Fft512 {
   template <int P, int C>
   __device__ static __forceinline__ void fwd_pass(double (&xr)[C][E], double (&xi)[C][E],
                                                   const double2 *tws, int lane) {
-    constexpr int s0 = P * R, lb = L - s0 - R;
 #pragma unroll
     for (int k = 0; k < R; ++k) {
       const int half = 1 << (R - 1 - k);
@@ -98,7 +115,6 @@ struct Fft512 {
   template <int P, int C>
   __device__ static __forceinline__ void inv_pass(double (&xr)[C][E], double (&xi)[C][E],
                                                   const double2 *tws, int lane) {
-    constexpr int s0 = P * R, lb = L - s0 - R;
 #pragma unroll
     for (int k = R - 1; k >= 0; --k) {
       const int half = 1 << (R - 1 - k);
@@ -119,26 +135,39 @@ struct Fft512 {
       }
     }
   }
-
+  // C transforms at once (lds holds C * N complex)
   template <int C>
   __device__ static __forceinline__ void fwd(double (&xr)[C][E], double (&xi)[C][E], double2 *lds,
                                              const double2 *tws, int lane) {
+    static_assert(NPASS <= 5, "unrolled for up to 5 passes");
     fwd_pass<0, C>(xr, xi, tws, lane);
-    exchange<C>(xr, xi, lds, lane, 0, 1);
-    fwd_pass<1, C>(xr, xi, tws, lane);
-    exchange<C>(xr, xi, lds, lane, 1, 2);
-    fwd_pass<2, C>(xr, xi, tws, lane);
+#define OMR_FFT_FWD_STEP(P)                            \
+  if constexpr (NPASS > P) {                           \
+    exchange<C>(xr, xi, lds, lane, P - 1, P);          \
+    fwd_pass<(NPASS > P ? P : 0), C>(xr, xi, tws, lane); \
+  }
+    OMR_FFT_FWD_STEP(1)
+    OMR_FFT_FWD_STEP(2)
+    OMR_FFT_FWD_STEP(3)
+    OMR_FFT_FWD_STEP(4)
+#undef OMR_FFT_FWD_STEP
   }
   template <int C>
   __device__ static __forceinline__ void inv(double (&xr)[C][E], double (&xi)[C][E], double2 *lds,
                                              const double2 *tws, int lane) {
-    inv_pass<2, C>(xr, xi, tws, lane);
-    exchange<C>(xr, xi, lds, lane, 2, 1);
-    inv_pass<1, C>(xr, xi, tws, lane);
-    exchange<C>(xr, xi, lds, lane, 1, 0);
+    static_assert(NPASS <= 5, "unrolled for up to 5 passes");
+#define OMR_FFT_INV_STEP(P)                            \
+  if constexpr (NPASS > P) {                           \
+    inv_pass<(NPASS > P ? P : 0), C>(xr, xi, tws, lane); \
+    exchange<C>(xr, xi, lds, lane, P, P - 1);          \
+  }
+    OMR_FFT_INV_STEP(4)
+    OMR_FFT_INV_STEP(3)
+    OMR_FFT_INV_STEP(2)
+    OMR_FFT_INV_STEP(1)
+#undef OMR_FFT_INV_STEP
     inv_pass<0, C>(xr, xi, tws, lane);
   }
-  // single transform
   __device__ static __forceinline__ void fwd(double (&xr)[E], double (&xi)[E], double2 *lds,
                                              const double2 *tws, int lane) {
     fwd<1>(reinterpret_cast<double(&)[1][E]>(xr), reinterpret_cast<double(&)[1][E]>(xi), lds, tws, lane);
@@ -148,5 +177,8 @@ struct Fft512 {
     inv<1>(reinterpret_cast<double(&)[1][E]>(xr), reinterpret_cast<double(&)[1][E]>(xi), lds, tws, lane);
   }
 };
+
+using Fft512 = WgFft<64, 8, 9>;     // level 1: N1 = 1024, one wave
+using Fft1024 = WgFft<256, 4, 10>;  // level 2: N2 = 2048, four waves
 
 }  // namespace omr

@@ -10,6 +10,10 @@
 
 #include "common.hpp"
 
+#ifndef OMR_DB_XCH
+#define OMR_DB_XCH 1  // NTT exchanges through two alternating LDS buffers (fewer barriers)
+#endif
+
 namespace omr {
 
 template <int LEVEL>
@@ -88,7 +92,10 @@ struct WgNtt {
   static constexpr int R = ilog2(E);
   static constexpr int NPASS = (L + R - 1) / R;
   static_assert(N == M::N, "NTT size mismatch");
-  static constexpr int LDS_DOUBLES = N;
+  // Exchanges alternate between two LDS buffers so only the last exchange of a transform needs
+  // the barrier after its reads (DB); lds then holds 2 * C * N doubles.
+  static constexpr bool DB = OMR_DB_XCH != 0;
+  static constexpr int LDS_DOUBLES = (DB ? 2 : 1) * N;
 
   // XOR swizzle of the exchange buffer: bank-conflict free for every (T, E) used here
   // (tools/lds_banks.py models the ds_read_b64 / ds_write_b64 lane groups).
@@ -110,19 +117,21 @@ struct WgNtt {
   }
 
   // ---- C independent transforms interleaved (C x E residues per thread, C LDS buffers) ----
+  // ordinal: index of this exchange within the transform; last: no further exchange follows.
   template <int C>
   __device__ static __forceinline__ void exchangeC(double (&x)[C][E], double *lds, int tid,
-                                                   int p_from, int p_to) {
+                                                   int p_from, int p_to, int ordinal, bool last) {
+    double *buf = lds + (DB ? (ordinal & 1) * C * N : 0);
 #pragma unroll
     for (int c = 0; c < C; ++c)
 #pragma unroll
-      for (int e = 0; e < E; ++e) lds[c * N + pad(index(p_from, tid, e))] = x[c][e];
+      for (int e = 0; e < E; ++e) buf[c * N + pad(index(p_from, tid, e))] = x[c][e];
     __syncthreads();
 #pragma unroll
     for (int c = 0; c < C; ++c)
 #pragma unroll
-      for (int e = 0; e < E; ++e) x[c][e] = lds[c * N + pad(index(p_to, tid, e))];
-    __syncthreads();
+      for (int e = 0; e < E; ++e) x[c][e] = buf[c * N + pad(index(p_to, tid, e))];
+    if (!DB || last) __syncthreads();
   }
 
   template <int P, int C>
@@ -197,7 +206,7 @@ struct WgNtt {
   __device__ static __forceinline__ void fwd_fromC(double (&x)[C][E], double *lds, const double *tw,
                                                    int tid, int &since_red) {
     if constexpr (P < NPASS) {
-      if constexpr (P > 0) exchangeC<C>(x, lds, tid, P - 1, P);
+      if constexpr (P > 0) exchangeC<C>(x, lds, tid, P - 1, P, P - 1, P == NPASS - 1);
       fwd_passC<P, C>(x, tw, tid, since_red);
       fwd_fromC<P + 1, C>(x, lds, tw, tid, since_red);
     }
@@ -206,13 +215,13 @@ struct WgNtt {
   __device__ static __forceinline__ void inv_fromC(double (&x)[C][E], double *lds, const double *itw,
                                                    int tid, int &since_red) {
     if constexpr (P >= 0) {
-      if constexpr (P < NPASS - 1) exchangeC<C>(x, lds, tid, P + 1, P);
+      if constexpr (P < NPASS - 1) exchangeC<C>(x, lds, tid, P + 1, P, NPASS - 2 - P, P == 0);
       inv_passC<P, C>(x, itw, tid, since_red);
       inv_fromC<P - 1, C>(x, lds, itw, tid, since_red);
     }
   }
 
-  // C transforms at once; lds holds C*N doubles. Bounds as for the single transforms.
+  // C transforms at once; lds holds C * LDS_DOUBLES doubles. Bounds as for the single transforms.
   template <int C>
   __device__ static __forceinline__ void fwdC(double (&x)[C][E], double *lds, const double *tw,
                                               int tid) {

@@ -39,6 +39,15 @@ namespace omr {
 #ifndef OMR_FFT1
 #define OMR_FFT1 1        // level 1: FP64 complex-FFT external product (br1_fft.hpp)
 #endif
+#ifdef OMR_EXPT_KEYWRAP  // timing experiment only (wrong results): L2-resident key rows
+#define OMR_KEYROW2(i) ((i) & 3)
+#else
+#define OMR_KEYROW2(i) (i)
+#endif
+#ifndef OMR_FFT2
+#define OMR_FFT2 0        // level 2: FP64 complex-FFT external product, 2-limb keys (br2_fft.hpp);
+                          // exact and tested, slower than the NTT at this geometry
+#endif
 #ifndef OMR_KEY_NT
 #define OMR_KEY_NT 0
 #endif
@@ -65,7 +74,7 @@ struct DeviceTables {
   const double *lut1, *lut2;              // LUTs, coefficient domain (centred)
   const uint16_t *trace_perm;             // [11][2048] NTT-domain permutation of sigma_g
   const uint16_t *trace_src;              // [11][2048] coefficient source index of sigma_g (+N: negate)
-  const double2 *fft1;                    // level-1 FFT twiddles (device_fft.hpp)
+  const double2 *fft1, *fft2;             // level-1 / level-2 FFT twiddles (device_fft.hpp)
 };
 
 // ---- key conversion: coefficient-domain canonical residues -> NTT-domain centred residues ----
