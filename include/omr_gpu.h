@@ -104,6 +104,28 @@ omr_status omr_payload_weights(const uint8_t seed[32], size_t all_payloads_count
                                uint32_t cmb_count_per_cipher, uint16_t *out);
 
 /* ---------------------------------------------------------------------------------------
+ * Retriever (client side, CPU): Retriever::decode_digest (retriever.rs:188-260).
+ * ------------------------------------------------------------------------------------- */
+/* Decrypt + decode n NttRlweCiphertexts (u64 [n][2][2048], NTT domain) under the pack's s2:
+ * out[m][j] = round_half_up(phase_j * 257 / q2) mod 257 (retriever.rs:84-96). */
+omr_status omr_decrypt_decode(const omr_secret_key_pack *sk, const uint64_t *ct, size_t n,
+                              uint32_t *out);
+/* decode_pertinent_indices over the index digest ciphertexts in order, stopping once
+ * pertinent_count distinct indices are known (retriever.rs:63-130, :197-201). Writes up to cap
+ * indices in increasing order and the number found (the caller compares it with the count). */
+omr_status omr_retrieve_indices(const omr_secret_key_pack *sk, const uint64_t *idx_cts,
+                                uint32_t n_ct, size_t all_payloads_count, size_t pertinent_count,
+                                size_t *indices, size_t cap, size_t *found);
+/* decode_combined_payloads + solve_matrix_mod_257 (retriever.rs:203-258, matrix.rs:164-247):
+ * payloads u16 [n_indices][612] of the sorted retrieved indices, from the payload digest
+ * ciphertexts and the board's weights (omr_payload_weights, same seed as the detector).
+ * OMR_ERR_NOT_INVERTIBLE when the system is singular. */
+omr_status omr_retrieve_payloads(const omr_secret_key_pack *sk, const uint64_t *pay_cts,
+                                 uint32_t n_ct, size_t all_payloads_count,
+                                 const uint16_t *weights, const size_t *indices, size_t n_indices,
+                                 uint16_t *payloads);
+
+/* ---------------------------------------------------------------------------------------
  * Detector — one context per GPU; calls on one context are serialised; contexts are
  * independent. Detector::new (detector.rs:85-110) uploads the keys and converts them to the
  * device layout; the LUTs (:457-503) are built inside.

@@ -48,3 +48,31 @@ def test_end_to_end_retrieval(oracle):
     solved = R.decode_payloads(s2, pay_cts, w, D, idx, rp.combination_count)
     for i, p in zip(idx, solved):
         assert p == payloads[i].tolist()
+
+
+def test_native_retriever_matches(oracle):
+    """The library's client-side retriever (retriever.hip, Retriever::decode_digest) on oracle
+    digests: same plaintexts as the test decoder, exact indices and payloads."""
+    a, _, _ = PL.keys()
+    s2 = a.export()["s2"]
+    D = 5
+    mask = np.array([1, 0, 0, 1, 1], dtype=bool)
+    ca, cb = PL.mixed_clues(mask, seed=31)
+    pv = oracle.detect_batch(ca, cb)
+    rng = np.random.default_rng(8)
+    payloads = rng.integers(0, 256, (D, 612)).astype(np.uint16)
+    rp = A.RetrievalParams(D, int(mask.sum()))
+    idx_cts = np.stack([O.encode_indices(pv, 0, D, 7, ct) for ct in range(rp.max_encode_indices_cipher_count)])
+    seed = bytes(range(100, 132))
+    w = A.payload_weights(seed, rp)
+    pay_cts = O.encode_payloads(pv, payloads, 0, D, w, rp.cmb_cipher_count, rp.cmb_count_per_cipher)
+    ret = A.Retriever(rp, a)
+    for ct in list(idx_cts[:1]) + list(pv[:2]):
+        assert np.array_equal(ret.decrypt_decode(ct)[0], R.decrypt_decode(s2, ct))
+    indices, pays = ret.decode_digest(idx_cts, pay_cts, seed)
+    assert indices == np.nonzero(mask)[0].tolist()
+    for i, p in zip(indices, pays):
+        assert p.tolist() == payloads[i].tolist()
+    # a singular system is reported, not silently solved (OmrError::InvertibleMatrix)
+    with pytest.raises(A.OmrError):
+        ret.decode_combined_payloads_and_solve(pay_cts, np.zeros_like(w), indices)

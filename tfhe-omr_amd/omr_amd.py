@@ -79,6 +79,13 @@ EXPORTS = {
     "omr_first_level": (C.c_int, [C.c_void_p, _u16p, _u16p, C.c_size_t, _u32p]),
     "omr_blind_rotate_level1": (C.c_int, [C.c_void_p, _u16p, _u16p, C.c_size_t, _u64p]),
     "omr_fft1_mul": (C.c_int, [C.c_void_p, _u32p, _u32p, C.c_size_t, _u64p]),
+    "omr_decrypt_decode": (C.c_int, [C.c_void_p, _u64p, C.c_size_t, _u32p]),
+    "omr_retrieve_indices": (C.c_int, [C.c_void_p, _u64p, C.c_uint32, C.c_size_t, C.c_size_t,
+                                       np.ctypeslib.ndpointer(dtype=np.uintp, flags="C_CONTIGUOUS"),
+                                       C.c_size_t, C.POINTER(C.c_size_t)]),
+    "omr_retrieve_payloads": (C.c_int, [C.c_void_p, _u64p, C.c_uint32, C.c_size_t, _u16p,
+                                        np.ctypeslib.ndpointer(dtype=np.uintp, flags="C_CONTIGUOUS"),
+                                        C.c_size_t, _u16p]),
     "omr_second_level": (C.c_int, [C.c_void_p, _u32p, C.c_size_t, _u64p]),
     "omr_blind_rotate_level2": (C.c_int, [C.c_void_p, _u32p, C.c_size_t, _u64p]),
     "omr_ntt": (C.c_int, [C.c_int, C.c_int, _u64p, C.c_size_t, C.c_int]),
@@ -191,6 +198,48 @@ class SecretKeyPack:
         _check(lib().omr_gen_clues(self._h, seed, first, count, a.reshape(-1), b.reshape(-1), nthreads),
                "omr_gen_clues")
         return a, b
+
+
+class Retriever:
+    """Retriever (retriever.rs:25-260): client-side digest decoding with the pack's s2 (CPU)."""
+
+    def __init__(self, params: RetrievalParams, secret: "SecretKeyPack"):
+        self.params = params
+        self._sk = secret
+
+    def decrypt_decode(self, cts) -> np.ndarray:
+        """Decoded plaintexts mod 257 of NttRlweCiphertexts u64 [n][2][2048]: u32 [n][2048]."""
+        cts = np.ascontiguousarray(cts, dtype=np.uint64).reshape(-1, 2, N2)
+        out = np.empty((cts.shape[0], N2), np.uint32)
+        _check(lib().omr_decrypt_decode(self._sk._h, cts.reshape(-1), cts.shape[0], out.reshape(-1)),
+               "omr_decrypt_decode")
+        return out
+
+    def decode_pertinent_indices(self, idx_cts) -> list[int]:
+        rp = self.params
+        cts = np.ascontiguousarray(idx_cts, dtype=np.uint64).reshape(-1, 2, N2)
+        buf = np.zeros(max(1, rp.pertinent_count) * 4 + 64, dtype=np.uintp)
+        found = C.c_size_t()
+        _check(lib().omr_retrieve_indices(self._sk._h, cts.reshape(-1), cts.shape[0], rp.all_payloads_count,
+                                          rp.pertinent_count, buf, buf.size, C.byref(found)),
+               "omr_retrieve_indices")
+        return [int(v) for v in buf[:min(found.value, buf.size)]]
+
+    def decode_combined_payloads_and_solve(self, pay_cts, weights, indices) -> np.ndarray:
+        rp = self.params
+        cts = np.ascontiguousarray(pay_cts, dtype=np.uint64).reshape(-1, 2, N2)
+        idx = np.ascontiguousarray(sorted(indices), dtype=np.uintp)
+        out = np.zeros((len(idx), PAYLOAD_LENGTH), np.uint16)
+        _check(lib().omr_retrieve_payloads(self._sk._h, cts.reshape(-1), cts.shape[0], rp.all_payloads_count,
+                                           np.ascontiguousarray(weights, dtype=np.uint16).reshape(-1), idx,
+                                           len(idx), out.reshape(-1)), "omr_retrieve_payloads")
+        return out
+
+    def decode_digest(self, idx_cts, pay_cts, seed: bytes):
+        """Retriever::decode_digest: sorted pertinent indices and their payloads (mod 257)."""
+        indices = self.decode_pertinent_indices(idx_cts)
+        weights = payload_weights(seed, RetrievalParams(self.params.all_payloads_count, len(indices)))
+        return indices, self.decode_combined_payloads_and_solve(pay_cts, weights, indices)
 
 
 class Detector:
