@@ -7,7 +7,13 @@ One step = one detect pass over the D clues of every rank. N > 1: one process pe
 (torch.distributed, RCCL), each rank owns a contiguous range of global message indices
 (weak scaling, no data-path collective). Rank 0 prints one JSON line.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--messages D]
+After the timed detect steps, one end-to-end pass (configs[4] shape) runs
+on the last pertinency vector: encode_pertinent_indices + encode_pertinent_payloads over each
+rank's shard with global indices, one RCCL reduce of the partial digests to rank 0, and the
+client-side retrieval (the library's Retriever) must recover exactly the pertinent indices and
+their payloads ("e2e" in the JSON line; --no-e2e skips it).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--messages D] [--no-e2e]
 """
 from __future__ import annotations
 
@@ -32,12 +38,15 @@ BR2_BYTES = 670 * 12 * 2 * 2048 * 8               # BSK2 (u64)               = 2
 TRACE_BYTES = 11 * 25 * 2 * 2048 * 8              # trace key (u64)          =   9,011,200
 IO_BYTES = 512 * 2 + 7 * 2 + 2 * 2048 * 8         # clue in + NttRlwe out    =      33,806
 DETECT_BYTES = BR1_BYTES + KS_BYTES + BR2_BYTES + TRACE_BYTES + IO_BYTES
-KERNEL_BYTES = {  # per message, per kernel of the pipeline
-    "br1_kernel": BR1_BYTES + 7 * (512 * 2 + 2) + 7 * 1025 * 4,
-    "ks_kernel": KS_BYTES + 1025 * 4 + 671 * 4,
-    "br2_trace_kernel": BR2_BYTES + TRACE_BYTES + 671 * 4 + 2 * 2048 * 8,
+KERNEL_BYTES = {  # per message, per pipeline stage (kernel names from A.detect_kernels())
+    "br1": BR1_BYTES + 7 * (512 * 2 + 2) + 7 * 1025 * 4,
+    "ks": KS_BYTES + 1025 * 4 + 671 * 4,
+    "br2": BR2_BYTES + TRACE_BYTES + 671 * 4 + 2 * 2048 * 8,
 }
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
+# FP64 VALU issue rate: 256 CUs x 4 SIMDs x 16 FP64 lanes x 2.4 GHz (78.6 TFLOP/s counting FMA as
+# 2); the arithmetic microbenchmark reaches 95 % of it (profiles/r01_microbench_arith.txt).
+FP64_PEAK_T_LANE_INSTR = 256 * 4 * 16 * 2.4e9 / 1e12
 PUBLISHED_CPU_MSG_S = 1e3 / 234.073003  # README.md:122, 1 thread AVX-512
 
 
@@ -51,6 +60,7 @@ def parse():
     ap.add_argument("--cpu-baseline-msgs", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-latency", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the encode + reduce + retrieval pass")
     return ap.parse_args()
 
 
@@ -72,15 +82,68 @@ def cpu_baseline(dk, ca, cb, nmsg):
             "sample": f"{nmsg} detect() calls of the same workload, OpenMP over messages, {dt:.1f}s wall"}
 
 
-def load_pmc_traffic():
-    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summary
-    (profiles/*pmc*.json, produced by tools/profile.sh on the GPU box), else None."""
-    path = os.path.join(ROOT, "profiles", "pmc_latest.json")
+def load_profile(name):
+    """A committed rocprofv3 summary under profiles/ (tools/profile.sh, tools/compute_summary.py)."""
+    path = os.path.join(ROOT, "profiles", name)
     if not os.path.exists(path):
-        return None, None
+        return None
     with open(path) as f:
-        d = json.load(f)
-    return d.get("kernel"), d
+        return json.load(f)
+
+
+def synthetic_payloads(first: int, count: int) -> np.ndarray:
+    """Payloads (payload.rs:26-38: 612 bytes) as a fixed function of the global message index,
+    so any rank (and the retrieval check) can regenerate them: u16 [count][612] in [0, 256)."""
+    i = np.arange(first, first + count, dtype=np.uint64)[:, None]
+    b = np.arange(612, dtype=np.uint64)[None, :]
+    h = i * np.uint64(0x9E3779B97F4A7C15) + b * np.uint64(0xBF58476D1CE4E5B9)
+    h ^= h >> np.uint64(31)
+    return ((h >> np.uint64(24)) & np.uint64(255)).astype(np.uint16)
+
+
+def end_to_end(det, pack_a, d_out, D, first, total, pert, dist, dev, stream, rank):
+    """encode_pertinent_indices + encode_pertinent_payloads over this shard (global indices),
+    one RCCL reduce to rank 0, then Retriever::decode_digest on rank 0 (examples/omr.rs:219-293)."""
+    import torch
+
+    rp = A.RetrievalParams(total, len(pert))
+    n_idx, n_pay, per = rp.max_encode_indices_cipher_count, rp.cmb_cipher_count, rp.cmb_count_per_cipher
+    seed = bytes(range(1, 33))
+    d_pay = torch.from_numpy(synthetic_payloads(first, D).view(np.int16)).to(dev)
+    d_w = torch.from_numpy(A.payload_weights(seed, rp).view(np.int16)).to(dev)
+    d_dig = torch.empty((n_idx + n_pay, 2, 2048), dtype=torch.int64, device=dev)
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    det.encode_indices_device(d_out.data_ptr(), D, first, total, 9, 0, n_idx, d_dig.data_ptr(), stream.cuda_stream)
+    det.encode_payloads_device(d_out.data_ptr(), d_pay.data_ptr(), D, first, total, d_w.data_ptr(), n_pay, per,
+                               d_dig[n_idx:].data_ptr(), stream.cuda_stream)
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    if dist:
+        dist.reduce(d_dig, dst=0, op=dist.ReduceOp.SUM)  # partial digests (< q2 each), int64 sum
+        torch.cuda.synchronize(dev)
+    t2 = time.perf_counter()
+    times = [t1 - t0, t2 - t0]
+    if dist:
+        tt = torch.tensor(times, dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        times = tt.tolist()
+    if rank != 0:
+        return None
+    digest = d_dig.cpu().numpy().view(np.uint64) % np.uint64(A.Q2)
+    t3 = time.perf_counter()
+    indices, pays = A.Retriever(rp, pack_a).decode_digest(digest[:n_idx], digest[n_idx:], seed)
+    t4 = time.perf_counter()
+    ok = indices == [int(v) for v in pert]
+    if ok:
+        want = np.concatenate([synthetic_payloads(int(i), 1) for i in indices]) if indices else np.zeros((0, 612))
+        ok = bool(np.array_equal(pays, want))
+    return {"ok": ok, "encode_ms": round(times[0] * 1e3, 2), "encode_reduce_ms": round(times[1] * 1e3, 2),
+            "retrieve_ms": round((t4 - t3) * 1e3, 2), "index_ct": n_idx, "payload_ct": n_pay,
+            "digest_bytes": int(d_dig.numel() * 8), "collective": "reduce(sum) over RCCL" if dist else "none",
+            "pertinent_recovered": len(indices)}
 
 
 def main():
@@ -155,18 +218,13 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
 
-    # correctness spot check on this rank's data (device result, client-side decrypt)
-    ok = True
-    try:
-        sys.path.insert(0, os.path.join(ROOT, "tests"))
-        import retriever as R
-        s2 = pack_a.export()["s2"]
-        host = d_out[: min(D, 256)].cpu().numpy().view(np.uint64)
-        for m in range(host.shape[0]):
-            dec = R.decrypt_decode(s2, host[m])
-            ok &= bool((dec[0] == 1) == mask[m]) and not dec[1:].any()
-    except Exception as e:  # noqa: BLE001
-        ok = f"check failed: {e}"
+    # correctness spot check on this rank's data: the client decrypts (library Retriever, CPU)
+    # and every pertinency ciphertext must decode to [1, 0, ..., 0] or all zeros (omd.rs:48-58)
+    host = d_out[: min(D, 256)].cpu().numpy().view(np.uint64)
+    dec = A.Retriever(A.RetrievalParams(max(1, D), 1), pack_a).decrypt_decode(host)
+    ok = bool(np.array_equal(dec[:, 0] == 1, mask[: host.shape[0]]) and not dec[:, 1:].any())
+
+    e2e = None if args.no_e2e else end_to_end(det, pack_a, d_out, D, first, total, pert, dist, dev, stream, rank)
 
     latency_ms = None
     if not args.no_latency:
@@ -187,19 +245,30 @@ def main():
 
     msgs = args.steps * D * world
     value = msgs / elapsed
-    # roofline of the dominant kernel: algorithmic bytes per launch / average launch duration
-    kms = {"br1_kernel": stage["first_level_ms"], "ks_kernel": stage["key_switch_ms"],
-           "br2_trace_kernel": stage["second_level_ms"]}
-    dom = max(kms, key=kms.get)
+    # roofline of the dominant kernel: algorithmic bytes per launch / average launch duration,
+    # both from HIP events the library records on `stream` around each launch
+    names = A.detect_kernels()
+    kms = {"br1": stage["first_level_ms"], "ks": stage["key_switch_ms"], "br2": stage["second_level_ms"]}
+    role = max(kms, key=kms.get)
+    dom = names[role]
     chunks = -(-D // 16384)
     launches = args.steps * chunks
-    avg_launch_s = kms[dom] / 1e3 / launches
+    avg_launch_s = kms[role] / 1e3 / launches
     per_launch_msgs = D / chunks
-    achieved = KERNEL_BYTES[dom] * per_launch_msgs / avg_launch_s / 1e9
-    pmc_kernel, pmc = load_pmc_traffic()
+    achieved = KERNEL_BYTES[role] * per_launch_msgs / avg_launch_s / 1e9
+    pmc = load_profile("pmc_latest.json")
     traffic = None
-    if pmc and pmc_kernel == dom and pmc.get("messages_per_launch"):
-        traffic = pmc["hbm_bytes_per_launch"] * per_launch_msgs / pmc["messages_per_launch"]
+    if pmc and dom in pmc.get("kernels", {}) and pmc.get("messages_per_launch"):
+        traffic = pmc["kernels"][dom]["hbm_bytes_per_launch"] * per_launch_msgs / pmc["messages_per_launch"]
+    comp = load_profile("compute_latest.json")
+    compute = None
+    if comp and dom in comp.get("kernels", {}):
+        lane_instr = comp["kernels"][dom]["fp64_lane_instr_per_msg"] * per_launch_msgs / avg_launch_s / 1e12
+        flops = comp["kernels"][dom]["fp64_flop_per_msg"] * per_launch_msgs / avg_launch_s / 1e12
+        compute = {"bound": "fp64-valu", "kernel": dom, "achieved": round(lane_instr, 2),
+                   "peak": round(FP64_PEAK_T_LANE_INSTR, 2), "unit": "T FP64 lane-instr/s",
+                   "frac": round(lane_instr / FP64_PEAK_T_LANE_INSTR, 4), "tflops": round(flops, 2),
+                   "counts_from": comp.get("source")}
     line = {
         "metric": "detect-phase messages/sec (D=65536 per GPU)",
         "value": round(value, 2),
@@ -225,7 +294,9 @@ def main():
                      "traffic": None if traffic is None else round(traffic),
                      "whole_detect_achieved": round(value / world * DETECT_BYTES / 1e9, 1),
                      "whole_detect_frac": round(value / world * DETECT_BYTES / 1e9 / HBM_PEAK_GBS, 4)},
+        "compute": compute,
         "correct": ok,
+        "e2e": e2e,
         "setup_s": round(setup_s, 1),
     }
     if not args.no_cpu_baseline and world == 1:

@@ -142,6 +142,8 @@ typedef struct {
 omr_status omr_ctx_create(const omr_detection_key_view *key, int device, omr_ctx **out);
 void omr_ctx_destroy(omr_ctx *ctx);
 /* Messages per internal batch (memory/latency knob); 0 = default. */
+/* Kernel names of this build's detect pipeline: "br1=<name> ks=<name> br2=<name>". */
+const char *omr_detect_kernels(void);
 omr_status omr_ctx_set_batch(omr_ctx *ctx, size_t batch);
 
 /* Detector::detect (detector.rs:135-166), batched like `par_iter().map(detect)` in

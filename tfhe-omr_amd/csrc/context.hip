@@ -124,6 +124,17 @@ struct omr_ctx {
   std::mutex mu;
 };
 
+#if OMR_FFT1
+#define OMR_BR1_NAME "br1f_kernel"
+#else
+#define OMR_BR1_NAME "br1_kernel"
+#endif
+#if OMR_FFT2
+#define OMR_BR2_NAME "br2f_trace_kernel"
+#else
+#define OMR_BR2_NAME "br2_trace_kernel"
+#endif
+
 namespace {
 
 omr_status ensure_batch(omr_ctx *c, size_t B) {
@@ -349,6 +360,11 @@ extern "C" void omr_ctx_destroy(omr_ctx *c) {
   for (auto e : c->events) hipEventDestroy(e);
   if (c->stream) hipStreamDestroy(c->stream);
   delete c;
+}
+
+// Names of the detect-path kernels this build launches (bench.py / profile summaries).
+extern "C" const char *omr_detect_kernels(void) {
+  return "br1=" OMR_BR1_NAME " ks=ks_kernel br2=" OMR_BR2_NAME;
 }
 
 extern "C" omr_status omr_ctx_set_batch(omr_ctx *c, size_t batch) {

@@ -53,6 +53,7 @@ class _Timing(C.Structure):
 EXPORTS = {
     "omr_last_error": (C.c_char_p, []),
     "omr_version": (C.c_char_p, []),
+    "omr_detect_kernels": (C.c_char_p, []),
     "omr_keygen_secret": (C.c_int, [C.c_uint64, C.POINTER(C.c_void_p)]),
     "omr_secret_destroy": (None, [C.c_void_p]),
     "omr_secret_export": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
@@ -200,6 +201,11 @@ class SecretKeyPack:
         return a, b
 
 
+def detect_kernels() -> dict:
+    """{'br1': name, 'ks': name, 'br2': name} of the kernels this build launches."""
+    return dict(kv.split("=") for kv in lib().omr_detect_kernels().decode().split())
+
+
 class Retriever:
     """Retriever (retriever.rs:25-260): client-side digest decoding with the pack's s2 (CPU)."""
 
@@ -329,6 +335,19 @@ class Detector:
         _check(lib().omr_encode_payloads(self._h, pv.reshape(-1), pay.reshape(-1), D, global_offset,
                                          rp.all_payloads_count, w, n_ct, per, out.reshape(-1)), "omr_encode_payloads")
         return out
+
+    # device-pointer variants (chaining on the caller's HIP stream; pointers are raw addresses)
+    def encode_indices_device(self, d_pv: int, D: int, global_offset: int, all_payloads_count: int, seed: int,
+                              first_ct: int, n_ct: int, d_out: int, stream: int = 0) -> None:
+        _check(lib().omr_encode_indices_device(self._h, d_pv, D, global_offset, all_payloads_count, seed, first_ct,
+                                               n_ct, d_out, stream or None), "omr_encode_indices_device")
+
+    def encode_payloads_device(self, d_pv: int, d_payloads: int, D: int, global_offset: int,
+                               all_payloads_count: int, d_weights: int, n_ct: int, per_ct: int, d_out: int,
+                               stream: int = 0) -> None:
+        _check(lib().omr_encode_payloads_device(self._h, d_pv, d_payloads, D, global_offset, all_payloads_count,
+                                                d_weights, n_ct, per_ct, d_out, stream or None),
+               "omr_encode_payloads_device")
 
     # ---- stage entry points (benches/two_level_bs.rs) ----
     def first_level(self, clue_a, clue_b) -> np.ndarray:
