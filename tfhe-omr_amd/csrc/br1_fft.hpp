@@ -20,6 +20,9 @@ namespace omr {
 #ifndef BR1F_WAVES
 #define BR1F_WAVES (BR1F_RW > 1 ? 1 : 2)  // waves per SIMD the register allocation targets
 #endif
+#ifndef BR1F_WPG
+#define BR1F_WPG 4  // level-1 waves (rotations) per workgroup, kept in lockstep per CMUX step
+#endif
 #ifndef BR1F_RW
 #define BR1F_RW 1  // level-1 rotations per wave (key rows shared, transforms interleaved)
 #endif
@@ -73,14 +76,14 @@ __device__ __forceinline__ void br1f_digits(const int (&ac)[2][16], int *st, int
   for (int p = 0; p < 2; ++p)
 #pragma unroll
     for (int i = 0; i < 16; ++i) st[p * N1 + acc_coef(lane, i)] = ac[p][i];
-  __syncthreads();
+  wave_lds_sync();
 #pragma unroll
   for (int p = 0; p < 2; ++p)
 #pragma unroll
     for (int i = 0; i < 16; ++i)
       pk[p][i] = Lvl1Int::digits(
           Lvl1Int::canon(Lvl1Int::rot_read(st + p * N1, acc_coef(lane, i), a) - ac[p][i]));
-  __syncthreads();
+  wave_lds_sync();
 }
 
 // One CMUX step for RW rotations held by this wave (all at the same key row i; a[r] may be 0,
@@ -153,27 +156,29 @@ __device__ __forceinline__ void br1f_step(int (&ac)[RW][2][16], double2 *xch, co
   }
 }
 
-// Level-1 blind rotations, RW per wave (one wave per workgroup); rotation g = wg * RW + r:
-// input either clue g % 7 of message g / 7 (lwe_a == nullptr) or LWE g. nrot bounds g.
+// Level-1 blind rotations: BR1F_WPG waves per workgroup, RW rotations per wave; rotation
+// g = (wg * BR1F_WPG + wave) * RW + r: clue g % 7 of message g / 7 (lwe_a == nullptr) or LWE g;
+// nrot bounds g. The transforms are wave-private (wave-level LDS sync); one workgroup barrier
+// per CMUX step keeps the waves in lockstep so they read each key row together (L1/L2 hits)
+// and share one twiddle table.
 template <int RW>
-__global__ __launch_bounds__(64, BR1F_WAVES) void br1f_kernel(const uint16_t *__restrict__ clue_a,
-                                                      const uint16_t *__restrict__ clue_b,
-                                                      const uint16_t *__restrict__ lwe_a,
-                                                      const uint16_t *__restrict__ lwe_b,
-                                                      const double2 *__restrict__ bskf, DeviceTables tb,
-                                                      uint32_t *__restrict__ ext,
-                                                      uint64_t *__restrict__ rlwe_out, int mode,
-                                                      size_t nrot) {
-  constexpr int NF = Fft512::N;
-  __shared__ double2 xch[RW * NF];
+__global__ __launch_bounds__(64 * BR1F_WPG, BR1F_WAVES) void br1f_kernel(
+    const uint16_t *__restrict__ clue_a, const uint16_t *__restrict__ clue_b,
+    const uint16_t *__restrict__ lwe_a, const uint16_t *__restrict__ lwe_b,
+    const double2 *__restrict__ bskf, DeviceTables tb, uint32_t *__restrict__ ext,
+    uint64_t *__restrict__ rlwe_out, int mode, size_t nrot) {
+  constexpr int NF = Fft512::N, W = BR1F_WPG;
+  __shared__ double2 xch_all[W][RW * NF];
   __shared__ double2 tws[NF];
-  __shared__ uint16_t la[RW][N0];
-  const int lane = threadIdx.x;
+  __shared__ uint16_t la_all[W][RW][N0];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  double2 *xch = xch_all[wave];
+  uint16_t(*la)[N0] = la_all[wave];
   int b[RW];
   size_t g[RW];
 #pragma unroll
   for (int r = 0; r < RW; ++r) {
-    g[r] = (size_t)blockIdx.x * RW + r;
+    g[r] = ((size_t)blockIdx.x * W + wave) * RW + r;
     const size_t gi = g[r] < nrot ? g[r] : nrot - 1;  // a tail slot recomputes the last rotation
     if (lwe_a == nullptr) {  // extract clue c of message m (CmLweCiphertext::extract_all, :514)
       const size_t m = gi / CLUES;
@@ -198,11 +203,11 @@ __global__ __launch_bounds__(64, BR1F_WAVES) void br1f_kernel(const uint16_t *__
       ac[r][1][i] = (int)canon_small<Mod<1>>(rot_read<N1>(tb.lut1, acc_coef(lane, i), r0));
     }
   }
-#pragma unroll
-  for (int e = 0; e < 8; ++e) tws[lane + 64 * e] = tb.fft1[lane + 64 * e];
+  for (int j = threadIdx.x; j < NF; j += 64 * W) tws[j] = tb.fft1[j];
   __syncthreads();
 #pragma unroll 1
   for (int i = 0; i < N0; ++i) {
+    if (W > 1) __syncthreads();  // lockstep: the waves read key row i together
     int a[RW], any = 0;
 #pragma unroll
     for (int r = 0; r < RW; ++r) {
@@ -223,7 +228,7 @@ __global__ __launch_bounds__(64, BR1F_WAVES) void br1f_kernel(const uint16_t *__
       int *st = reinterpret_cast<int *>(xch + r * NF);
 #pragma unroll
       for (int i = 0; i < 16; ++i) st[acc_coef(lane, i)] = ac[r][0][i];
-      __syncthreads();
+      wave_lds_sync();
       uint32_t *o = ext + g[r] * (N1 + 1);
 #pragma unroll
       for (int i = 0; i < 16; ++i) {

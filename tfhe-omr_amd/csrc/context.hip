@@ -202,7 +202,8 @@ omr_status launch_br1(omr_ctx *c, size_t n, const uint16_t *ca, const uint16_t *
                       const uint16_t *la, const uint16_t *lb, uint32_t *ext, uint64_t *rlwe, int mode,
                       hipStream_t st) {
 #if OMR_FFT1
-  br1f_kernel<BR1F_RW><<<(unsigned)((n + BR1F_RW - 1) / BR1F_RW), 64, 0, st>>>(
+  constexpr size_t per_wg = (size_t)BR1F_RW * BR1F_WPG;
+  br1f_kernel<BR1F_RW><<<(unsigned)((n + per_wg - 1) / per_wg), 64 * BR1F_WPG, 0, st>>>(
       ca, cb, la, lb, c->bsk1f, c->tb, ext, rlwe, mode, n);
 #else
   br1_kernel<<<(unsigned)n, BR1_T, 0, st>>>(ca, cb, la, lb, c->bsk1, c->tb, ext, rlwe, mode);

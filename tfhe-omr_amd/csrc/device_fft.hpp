@@ -30,6 +30,22 @@
 
 namespace omr {
 
+// LDS visibility within one wave: wait for this wave's LDS operations and keep the compiler
+// from moving memory operations across (waves of a workgroup stay independent).
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+  __builtin_amdgcn_wave_barrier();
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+}
+// Transforms owned by one wave (T == 64) synchronise the wave only; larger ones the workgroup.
+template <int T>
+__device__ __forceinline__ void fft_sync() {
+  if constexpr (T == 64)
+    wave_lds_sync();
+  else
+    __syncthreads();
+}
+
 template <int T, int E, int L>
 struct FftSwizzle;
 template <>
@@ -77,7 +93,7 @@ struct WgFft {
 #pragma unroll
       for (int e = 0; e < E; ++e)
         lds[c * N + swz(index(p_from, lane, e))] = make_double2(xr[c][e], xi[c][e]);
-    __syncthreads();
+    fft_sync<T>();
 #pragma unroll
     for (int c = 0; c < C; ++c)
 #pragma unroll
@@ -86,7 +102,7 @@ struct WgFft {
         xr[c][e] = v.x;
         xi[c][e] = v.y;
       }
-    __syncthreads();
+    fft_sync<T>();
   }
 
   template <int P, int C>
