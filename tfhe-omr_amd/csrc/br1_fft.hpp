@@ -98,7 +98,7 @@ __device__ __forceinline__ void br1f_step(int (&ac)[RW][2][16], double2 *xch, co
   uint32_t pk[RW][2][16];
 #pragma unroll
   for (int r = 0; r < RW; ++r)
-    br1f_digits(ac[r], reinterpret_cast<int *>(xch + r * NF), a[r], lane, pk[r]);
+    br1f_digits(ac[r], reinterpret_cast<int *>(xch + r * F::BUF), a[r], lane, pk[r]);
 
   double outr[2][RW][8], outi[2][RW][8];  // [output A/B][rotation][point]
 #pragma unroll
@@ -168,7 +168,7 @@ __global__ __launch_bounds__(64 * BR1F_WPG, BR1F_WAVES) void br1f_kernel(
     const double2 *__restrict__ bskf, DeviceTables tb, uint32_t *__restrict__ ext,
     uint64_t *__restrict__ rlwe_out, int mode, size_t nrot) {
   constexpr int NF = Fft512::N, W = BR1F_WPG;
-  __shared__ double2 xch_all[W][RW * NF];
+  __shared__ double2 xch_all[W][RW * Fft512::BUF];
   __shared__ double2 tws[NF];
   __shared__ uint16_t la_all[W][RW][N0];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -225,7 +225,7 @@ __global__ __launch_bounds__(64 * BR1F_WPG, BR1F_WAVES) void br1f_kernel(
   for (int r = 0; r < RW; ++r) {
     if (g[r] >= nrot) break;
     if (mode == 0) {  // extract_lwe_locally (coefficient 0), detector.rs:561
-      int *st = reinterpret_cast<int *>(xch + r * NF);
+      int *st = reinterpret_cast<int *>(xch + r * Fft512::BUF);
 #pragma unroll
       for (int i = 0; i < 16; ++i) st[acc_coef(lane, i)] = ac[r][0][i];
       wave_lds_sync();
@@ -252,7 +252,7 @@ __global__ __launch_bounds__(64) void key_to_fft1_kernel(const uint32_t *__restr
                                                          double2 *__restrict__ out, size_t npoly,
                                                          const double2 *__restrict__ tw) {
   using F = Fft512;
-  __shared__ double2 xch[F::N];
+  __shared__ double2 xch[F::BUF];
   __shared__ double2 tws[F::N];
   const int lane = threadIdx.x;
   const size_t poly = blockIdx.x;
@@ -279,7 +279,7 @@ __global__ __launch_bounds__(64) void fft1_mul_kernel(const uint32_t *__restrict
                                                       uint64_t *__restrict__ out,
                                                       const double2 *__restrict__ tw) {
   using F = Fft512;
-  __shared__ double2 xch[F::N];
+  __shared__ double2 xch[F::BUF];
   __shared__ double2 tws[F::N];
   const int lane = threadIdx.x;
   const size_t poly = blockIdx.x;

@@ -28,6 +28,10 @@
 
 #include "device_ntt.hpp"
 
+#ifndef OMR_FFT1_PAD_ADD
+#define OMR_FFT1_PAD_ADD 0  // level-1 FFT exchanges: additive padding (no spills, but slower: DESIGN §7)
+#endif
+
 namespace omr {
 
 // LDS visibility within one wave: wait for this wave's LDS operations and keep the compiler
@@ -46,15 +50,24 @@ __device__ __forceinline__ void fft_sync() {
     __syncthreads();
 }
 
+// LDS exchange layout per geometry. ADD: additive padding slot(j) = j + (j >> PS), separable
+// over the disjoint lane / element fields of an exchange index, so every access is one per-lane
+// base register plus an immediate offset (tools/fft_lds_pad.py: 96 extra conflict cycles over
+// all patterns for 64x8). Otherwise an XOR swizzle slot(j) = j ^ f(j) with no conflicts
+// (tools/fft_lds_banks.py), at the cost of per-element address registers.
 template <int T, int E, int L>
 struct FftSwizzle;
 template <>
-struct FftSwizzle<64, 8, 9> {  // tools/fft_lds_banks.py 64 8 9
+struct FftSwizzle<64, 8, 9> {  // tools/fft_lds_banks.py 64 8 9; tools/fft_lds_pad.py 64 8 9
   static constexpr int M[6] = {4, 9, 15, 14, 0, 8};
+  static constexpr bool ADD = OMR_FFT1_PAD_ADD != 0;
+  static constexpr int PS = 3;
 };
 template <>
 struct FftSwizzle<256, 4, 10> {  // tools/fft_lds_banks.py 256 4 10
   static constexpr int M[7] = {2, 13, 6, 0, 4, 4, 2};
+  static constexpr bool ADD = false;
+  static constexpr int PS = 0;
 };
 
 template <int T_, int E_, int L_>
@@ -75,6 +88,20 @@ struct WgFft {
   __device__ static __forceinline__ int swz(int j) {
     return j ^ swz_bits(j, std::make_integer_sequence<int, L - 3>{});
   }
+  static constexpr bool ADD = FftSwizzle<T, E, L>::ADD;
+  static constexpr int PS = FftSwizzle<T, E, L>::PS;
+  static constexpr int BUF = ADD ? N + (N >> PS) : N;  // LDS slots (double2) per transform
+  // slot of register e of `lane` in pass p
+  __device__ static __forceinline__ int slot(int p, int lane, int e) {
+    if constexpr (ADD) {
+      const int lb = L - (p + 1) * R;
+      const int lp = ((lane >> lb) << (L - p * R)) | (lane & ((1 << lb) - 1));
+      const int ep = e << lb;
+      return (lp + (lp >> PS)) + (ep + (ep >> PS));  // = j + (j >> PS), fields disjoint
+    } else {
+      return swz(index(p, lane, e));
+    }
+  }
   // Node twiddle of stage P*R + k for register e. The last pass's stages are stored lane-minor
   // (entry (1 << s) + j * T + lane holds node (lane << k) + j) so a wave reads consecutive
   // entries; in earlier passes lanes of a group share (broadcast) entries.
@@ -92,13 +119,13 @@ struct WgFft {
     for (int c = 0; c < C; ++c)
 #pragma unroll
       for (int e = 0; e < E; ++e)
-        lds[c * N + swz(index(p_from, lane, e))] = make_double2(xr[c][e], xi[c][e]);
+        lds[c * BUF + slot(p_from, lane, e)] = make_double2(xr[c][e], xi[c][e]);
     fft_sync<T>();
 #pragma unroll
     for (int c = 0; c < C; ++c)
 #pragma unroll
       for (int e = 0; e < E; ++e) {
-        const double2 v = lds[c * N + swz(index(p_to, lane, e))];
+        const double2 v = lds[c * BUF + slot(p_to, lane, e)];
         xr[c][e] = v.x;
         xi[c][e] = v.y;
       }
@@ -151,7 +178,7 @@ struct WgFft {
       }
     }
   }
-  // C transforms at once (lds holds C * N complex)
+  // C transforms at once (lds holds C * BUF complex)
   template <int C>
   __device__ static __forceinline__ void fwd(double (&xr)[C][E], double (&xi)[C][E], double2 *lds,
                                              const double2 *tws, int lane) {
