@@ -23,6 +23,9 @@ namespace omr {
 #ifndef BR1F_WPG
 #define BR1F_WPG 4  // level-1 waves (rotations) per workgroup, kept in lockstep per CMUX step
 #endif
+#ifndef BR1F_KEY_LDS
+#define BR1F_KEY_LDS 1  // key rows staged through LDS by LDS-DMA, shared by the workgroup
+#endif
 #ifndef BR1F_RW
 #define BR1F_RW 1  // level-1 rotations per wave (key rows shared, transforms interleaved)
 #endif
@@ -116,6 +119,11 @@ __device__ __forceinline__ void br1f_step(int (&ac)[RW][2][16], double2 *xch, co
       double2 ka[8], kb[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
+#ifdef OMR_EXPT_NO_KEY  // timing experiment only (wrong results): no key loads
+        ka[e] = make_double2(1.0 + e, 2.0 - k);
+        kb[e] = make_double2(3.0 - e, 1.0 + k);
+        continue;
+#endif
         ka[e] = kr[e];
         if (!BR1F_KEY_SPLIT) kb[e] = kr[NF + e];
       }
@@ -128,10 +136,12 @@ __device__ __forceinline__ void br1f_step(int (&ac)[RW][2][16], double2 *xch, co
           xi[r][e] = Lvl1Int::digit(pk[r][p][8 + e], k);
         }
       F::fwd<RW>(xr, xi, xch, tws, lane);
+#ifndef OMR_EXPT_NO_KEY
       if (BR1F_KEY_SPLIT) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) kb[e] = kr[NF + e];
       }
+#endif
 #pragma unroll
       for (int r = 0; r < RW; ++r)
 #pragma unroll
@@ -156,6 +166,94 @@ __device__ __forceinline__ void br1f_step(int (&ac)[RW][2][16], double2 *xch, co
   }
 }
 
+// ---- key rows staged through LDS by LDS-DMA (BR1F_KEY_LDS) ----------------------------------
+// GGSW row q (global row index over the whole key: step * 8 + row) = [A/B][512] complex, 16 KB,
+// copied by the workgroup's waves with global_load_lds_dwordx4 into one of two LDS buffers,
+// transposed so that slot comp * 512 + e * 64 + lane holds the lane's e-th point (the
+// multiply-accumulate then reads consecutive slots: no bank conflicts). Each wave issues
+// 16 / BR1F_WPG of the row's 16 one-KiB instructions. Raw s_barrier + counted vmcnt keep the
+// next row's copy in flight across the barriers (cdna_hip_programming.md, "Pipelining across
+// barriers").
+constexpr int KROW_SLOTS = 2 * Fft512::N;  // double2 per staged row
+constexpr int KROW_INSTR = 16 / BR1F_WPG;  // glds per wave per row
+
+__device__ __forceinline__ void krow_issue(const double2 *__restrict__ row, double2 *buf, int lane,
+                                           int wave) {
+#pragma unroll
+  for (int u = 0; u < KROW_INSTR; ++u) {
+    const int ins = wave * KROW_INSTR + u;  // 0..15: comp = ins / 8, point e = ins % 8
+    const int comp = ins >> 3, e = ins & 7;
+    const double2 *src = row + comp * Fft512::N + lane * 8 + e;
+    __builtin_amdgcn_global_load_lds(src, buf + comp * Fft512::N + e * 64, 16, 0, 0);
+  }
+}
+__device__ __forceinline__ void vm_wait_row_in_flight() {  // s_waitcnt vmcnt(KROW_INSTR)
+  __builtin_amdgcn_s_waitcnt((KROW_INSTR & 0xF) | ((KROW_INSTR >> 4) << 14) | (0x7 << 4) | (0xF << 8));
+}
+__device__ __forceinline__ void vm_wait_all() {  // s_waitcnt vmcnt(0)
+  __builtin_amdgcn_s_waitcnt((0x7 << 4) | (0xF << 8));
+}
+__device__ __forceinline__ void wg_barrier_lds() {  // LDS reads/writes done, then s_barrier
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+  __builtin_amdgcn_s_barrier();
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+}
+
+// One CMUX step with LDS-staged key rows. q0 = first global row of this step; rows q0..q0+7 are
+// consumed, row q0+8 (next step's first) is prefetched at the end. kbuf: 2 staged rows.
+__device__ __forceinline__ void br1f_step_lds(int (&ac)[2][16], double2 *xch, const double2 *tws,
+                                              int a, const double2 *__restrict__ bskf, int q0,
+                                              int qtotal, double2 *kbuf, int lane, int wave) {
+  using F = Fft512;
+  uint32_t pk[2][16];
+  br1f_digits(ac, reinterpret_cast<int *>(xch), a, lane, pk);
+  double outr[2][8], outi[2][8];
+#pragma unroll
+  for (int o = 0; o < 2; ++o)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) outr[o][e] = outi[o][e] = 0.0;
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+#pragma unroll 1
+    for (int k = 0; k < D1; ++k) {
+      const int q = q0 + p * D1 + k;
+      wg_barrier_lds();  // every wave has finished reading buffer (q + 1) & 1 (row q - 1)
+      const bool more = q + 1 < qtotal;
+      if (more) krow_issue(bskf + (size_t)(q + 1) * KROW_SLOTS, kbuf + ((q + 1) & 1) * KROW_SLOTS, lane, wave);
+      double xr[8], xi[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        xr[e] = Lvl1Int::digit(pk[p][e], k);
+        xi[e] = Lvl1Int::digit(pk[p][8 + e], k);
+      }
+      F::fwd(xr, xi, xch, tws, lane);
+      if (more)
+        vm_wait_row_in_flight();  // row q landed (row q + 1 may stay in flight)
+      else
+        vm_wait_all();
+      wg_barrier_lds();  // ... in every wave's share
+      const double2 *kb = kbuf + (q & 1) * KROW_SLOTS;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const double2 ka = kb[e * 64 + lane], kB = kb[F::N + e * 64 + lane];
+        outr[0][e] = __fma_rn(xr[e], ka.x, __fma_rn(-xi[e], ka.y, outr[0][e]));
+        outi[0][e] = __fma_rn(xr[e], ka.y, __fma_rn(xi[e], ka.x, outi[0][e]));
+        outr[1][e] = __fma_rn(xr[e], kB.x, __fma_rn(-xi[e], kB.y, outr[1][e]));
+        outi[1][e] = __fma_rn(xr[e], kB.y, __fma_rn(xi[e], kB.x, outi[1][e]));
+      }
+    }
+  }
+#pragma unroll
+  for (int o = 0; o < 2; ++o) {
+    F::inv(outr[o], outi[o], xch, tws, lane);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const double v = rint(i < 8 ? outr[o][i] : outi[o][i - 8]);  // exact (< 2^43)
+      ac[o][i] = Lvl1Int::canon(ac[o][i] + (int)red<Mod<1>>(v));
+    }
+  }
+}
+
 // Level-1 blind rotations: BR1F_WPG waves per workgroup, RW rotations per wave; rotation
 // g = (wg * BR1F_WPG + wave) * RW + r: clue g % 7 of message g / 7 (lwe_a == nullptr) or LWE g;
 // nrot bounds g. The transforms are wave-private (wave-level LDS sync); one workgroup barrier
@@ -171,6 +269,10 @@ __global__ __launch_bounds__(64 * BR1F_WPG, BR1F_WAVES) void br1f_kernel(
   __shared__ double2 xch_all[W][RW * Fft512::BUF];
   __shared__ double2 tws[NF];
   __shared__ uint16_t la_all[W][RW][N0];
+#if BR1F_KEY_LDS
+  static_assert(RW == 1 && 16 % W == 0, "LDS key staging: one rotation per wave, W divides 16");
+  __shared__ double2 kbuf[2 * KROW_SLOTS];
+#endif
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   double2 *xch = xch_all[wave];
   uint16_t(*la)[N0] = la_all[wave];
@@ -205,6 +307,18 @@ __global__ __launch_bounds__(64 * BR1F_WPG, BR1F_WAVES) void br1f_kernel(
   }
   for (int j = threadIdx.x; j < NF; j += 64 * W) tws[j] = tb.fft1[j];
   __syncthreads();
+#if BR1F_KEY_LDS
+  // every step runs (a = 0 gives zero digits and leaves ACC unchanged) so the waves share the
+  // staged key rows; row 0 is issued before the loop
+  krow_issue(bskf, kbuf, lane, wave);
+#pragma unroll 1
+  for (int i = 0; i < N0; ++i) {
+    int a[RW];
+    a[0] = __builtin_amdgcn_readfirstlane(la[0][i]);
+    br1f_step_lds(ac[0], xch, tws, a[0], bskf, i * 2 * D1, N0 * 2 * D1, kbuf, lane, wave);
+  }
+  __syncthreads();
+#else
 #pragma unroll 1
   for (int i = 0; i < N0; ++i) {
     if (W > 1) __syncthreads();  // lockstep: the waves read key row i together
@@ -221,6 +335,7 @@ __global__ __launch_bounds__(64 * BR1F_WPG, BR1F_WAVES) void br1f_kernel(
     br1f_step<RW>(ac, xch, tws, a, bskf + (size_t)i * (2 * D1 * 2 * NF), lane);
 #endif
   }
+#endif
 #pragma unroll
   for (int r = 0; r < RW; ++r) {
     if (g[r] >= nrot) break;

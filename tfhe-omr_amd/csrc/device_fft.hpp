@@ -115,6 +115,9 @@ struct WgFft {
   template <int C>
   __device__ static __forceinline__ void exchange(double (&xr)[C][E], double (&xi)[C][E],
                                                   double2 *lds, int lane, int p_from, int p_to) {
+#ifdef OMR_EXPT_NO_EXCH  // timing experiment only (wrong results): no LDS exchange
+    return;
+#endif
 #pragma unroll
     for (int c = 0; c < C; ++c)
 #pragma unroll
@@ -132,16 +135,30 @@ struct WgFft {
     fft_sync<T>();
   }
 
-  template <int P, int C>
+  // Pass 0's node index does not depend on the lane (lane >> (L - R) == 0), so its twiddles
+  // are read from the global table with uniform addresses (scalar loads kept in SGPRs) when
+  // gtw is given; later passes read the LDS copy.
+  template <int P, bool G>
+  __device__ static __forceinline__ double2 twiddle(const double2 *tws, const double2 *__restrict__ gtw,
+                                                    int k, int e, int lane) {
+    if constexpr (P == 0 && G) return gtw[(1 << k) + (e >> (R - k))];
+#ifdef OMR_EXPT_TW_CONST  // timing experiment only (wrong results): no twiddle loads
+    return make_double2(0.70710678118654752 + k, 0.70710678118654752 - e);
+#endif
+    return tws[twiddle_index<P>(k, e, lane)];
+  }
+
+  template <int P, int C, bool G = false>
   __device__ static __forceinline__ void fwd_pass(double (&xr)[C][E], double (&xi)[C][E],
-                                                  const double2 *tws, int lane) {
+                                                  const double2 *tws, int lane,
+                                                  const double2 *__restrict__ gtw = nullptr) {
 #pragma unroll
     for (int k = 0; k < R; ++k) {
       const int half = 1 << (R - 1 - k);
 #pragma unroll
       for (int e = 0; e < E; ++e) {
         if (e & half) continue;
-        const double2 w = tws[twiddle_index<P>(k, e, lane)];
+        const double2 w = twiddle<P, G>(tws, gtw, k, e, lane);
 #pragma unroll
         for (int c = 0; c < C; ++c) {
           const double vr = __fma_rn(xr[c][e + half], w.x, -xi[c][e + half] * w.y);
@@ -155,16 +172,17 @@ struct WgFft {
       }
     }
   }
-  template <int P, int C>
+  template <int P, int C, bool G = false>
   __device__ static __forceinline__ void inv_pass(double (&xr)[C][E], double (&xi)[C][E],
-                                                  const double2 *tws, int lane) {
+                                                  const double2 *tws, int lane,
+                                                  const double2 *__restrict__ gtw = nullptr) {
 #pragma unroll
     for (int k = R - 1; k >= 0; --k) {
       const int half = 1 << (R - 1 - k);
 #pragma unroll
       for (int e = 0; e < E; ++e) {
         if (e & half) continue;
-        const double2 w = tws[twiddle_index<P>(k, e, lane)];
+        const double2 w = twiddle<P, G>(tws, gtw, k, e, lane);
 #pragma unroll
         for (int c = 0; c < C; ++c) {
           const double ur = xr[c][e], ui = xi[c][e];
@@ -179,11 +197,13 @@ struct WgFft {
     }
   }
   // C transforms at once (lds holds C * BUF complex)
-  template <int C>
+  // G: pass-0 twiddles from the global table gtw (must be non-null)
+  template <int C, bool G = false>
   __device__ static __forceinline__ void fwd(double (&xr)[C][E], double (&xi)[C][E], double2 *lds,
-                                             const double2 *tws, int lane) {
+                                             const double2 *tws, int lane,
+                                             const double2 *__restrict__ gtw = nullptr) {
     static_assert(NPASS <= 5, "unrolled for up to 5 passes");
-    fwd_pass<0, C>(xr, xi, tws, lane);
+    fwd_pass<0, C, G>(xr, xi, tws, lane, gtw);
 #define OMR_FFT_FWD_STEP(P)                            \
   if constexpr (NPASS > P) {                           \
     exchange<C>(xr, xi, lds, lane, P - 1, P);          \
@@ -195,9 +215,10 @@ struct WgFft {
     OMR_FFT_FWD_STEP(4)
 #undef OMR_FFT_FWD_STEP
   }
-  template <int C>
+  template <int C, bool G = false>
   __device__ static __forceinline__ void inv(double (&xr)[C][E], double (&xi)[C][E], double2 *lds,
-                                             const double2 *tws, int lane) {
+                                             const double2 *tws, int lane,
+                                             const double2 *__restrict__ gtw = nullptr) {
     static_assert(NPASS <= 5, "unrolled for up to 5 passes");
 #define OMR_FFT_INV_STEP(P)                            \
   if constexpr (NPASS > P) {                           \
@@ -209,14 +230,16 @@ struct WgFft {
     OMR_FFT_INV_STEP(2)
     OMR_FFT_INV_STEP(1)
 #undef OMR_FFT_INV_STEP
-    inv_pass<0, C>(xr, xi, tws, lane);
+    inv_pass<0, C, G>(xr, xi, tws, lane, gtw);
   }
   __device__ static __forceinline__ void fwd(double (&xr)[E], double (&xi)[E], double2 *lds,
-                                             const double2 *tws, int lane) {
+                                             const double2 *tws, int lane,
+                                             const double2 *__restrict__ gtw = nullptr) {
     fwd<1>(reinterpret_cast<double(&)[1][E]>(xr), reinterpret_cast<double(&)[1][E]>(xi), lds, tws, lane);
   }
   __device__ static __forceinline__ void inv(double (&xr)[E], double (&xi)[E], double2 *lds,
-                                             const double2 *tws, int lane) {
+                                             const double2 *tws, int lane,
+                                             const double2 *__restrict__ gtw = nullptr) {
     inv<1>(reinterpret_cast<double(&)[1][E]>(xr), reinterpret_cast<double(&)[1][E]>(xi), lds, tws, lane);
   }
 };
