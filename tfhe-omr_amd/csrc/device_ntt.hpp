@@ -10,6 +10,9 @@
 
 #include "common.hpp"
 
+#ifndef OMR_NTT_WAVE_LOCAL
+#define OMR_NTT_WAVE_LOCAL 1  // wave-level sync for NTT exchanges that stay inside each wave
+#endif
 #ifndef OMR_DB_XCH
 #define OMR_DB_XCH 1  // NTT exchanges through two alternating LDS buffers (fewer barriers)
 #endif
@@ -117,21 +120,59 @@ struct WgNtt {
   }
 
   // ---- C independent transforms interleaved (C x E residues per thread, C LDS buffers) ----
-  // ordinal: index of this exchange within the transform; last: no further exchange follows.
-  template <int C>
-  __device__ static __forceinline__ void exchangeC(double (&x)[C][E], double *lds, int tid,
-                                                   int p_from, int p_to, int ordinal, bool last) {
-    double *buf = lds + (DB ? (ordinal & 1) * C * N : 0);
+  // Thread owning element idx in pass p (inverse of index()).
+  static constexpr int thread_of(int p, int idx) {
+    const int s0 = p * R;
+    const int r = (L - s0) < R ? (L - s0) : R;
+    const int lb = L - s0 - r;
+    const int F = ((idx >> (L - s0)) << lb) | (idx & ((1 << lb) - 1));
+    return F >> (R - r);
+  }
+  // True when every element stays in the same wave between passes pf and pt: the exchange then
+  // needs only wave-level LDS synchronisation (each wave touches its own slots: pad() keeps the
+  // high index bits that select the wave).
+  static constexpr bool wave_local(int pf, int pt) {
+    if (T <= 64) return true;
+    for (int idx = 0; idx < N; ++idx)
+      if ((thread_of(pf, idx) >> 6) != (thread_of(pt, idx) >> 6)) return false;
+    return true;
+  }
+  __device__ static __forceinline__ void wave_sync() {
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+    __builtin_amdgcn_wave_barrier();
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  }
+
+  // Exchange PF -> PT, the ORD-th of its transform; LAST: no further exchange follows (a
+  // workgroup barrier then protects the buffers for whatever the caller does next).
+  // PREV_WL: the previous exchange of this transform was wave-local, so waves may still be
+  // reading their own slots; a cross-wave exchange must then wait for all of them first.
+  template <int C, int PF, int PT, int ORD, bool LAST, bool PREV_WL>
+  __device__ static __forceinline__ void exchangeC(double (&x)[C][E], double *lds, int tid) {
+#ifdef OMR_EXPT_NTT_NO_EXCH  // timing experiment only (wrong results)
+    return;
+#endif
+    constexpr bool WL = wave_local(PF, PT) && OMR_NTT_WAVE_LOCAL;
+    if constexpr (!WL && PREV_WL && OMR_NTT_WAVE_LOCAL) __syncthreads();
+    double *buf = lds + (DB ? (ORD & 1) * C * N : 0);
 #pragma unroll
     for (int c = 0; c < C; ++c)
 #pragma unroll
-      for (int e = 0; e < E; ++e) buf[c * N + pad(index(p_from, tid, e))] = x[c][e];
-    __syncthreads();
+      for (int e = 0; e < E; ++e) buf[c * N + pad(index(PF, tid, e))] = x[c][e];
+    if constexpr (WL)
+      wave_sync();
+    else
+      __syncthreads();
 #pragma unroll
     for (int c = 0; c < C; ++c)
 #pragma unroll
-      for (int e = 0; e < E; ++e) x[c][e] = buf[c * N + pad(index(p_to, tid, e))];
-    if (!DB || last) __syncthreads();
+      for (int e = 0; e < E; ++e) x[c][e] = buf[c * N + pad(index(PT, tid, e))];
+    if constexpr (LAST || !DB) {
+      if constexpr (!LAST && WL)
+        wave_sync();
+      else
+        __syncthreads();
+    }
   }
 
   template <int P, int C>
@@ -155,7 +196,11 @@ struct WgNtt {
         if (ep & half) continue;
         const int F = (tid << (R - r)) | (e >> r);
         const int hi = F >> lb;
+#ifdef OMR_EXPT_NTT_TW_CONST  // timing experiment only (wrong results)
+        const double w = 1234567.0 + s * 3 + e;
+#else
         const double w = tw[(1 << s) + ((hi << k) | (ep >> (r - k)))];
+#endif
 #pragma unroll
         for (int c = 0; c < C; ++c) {
           const double u = x[c][e];
@@ -189,7 +234,11 @@ struct WgNtt {
         if (ep & half) continue;
         const int F = (tid << (R - r)) | (e >> r);
         const int hi = F >> lb;
+#ifdef OMR_EXPT_NTT_TW_CONST  // timing experiment only (wrong results)
+        const double w = 7654321.0 + s * 3 + e;
+#else
         const double w = itw[(1 << s) + ((hi << k) | (ep >> (r - k)))];
+#endif
 #pragma unroll
         for (int c = 0; c < C; ++c) {
           const double u = x[c][e];
@@ -206,7 +255,8 @@ struct WgNtt {
   __device__ static __forceinline__ void fwd_fromC(double (&x)[C][E], double *lds, const double *tw,
                                                    int tid, int &since_red) {
     if constexpr (P < NPASS) {
-      if constexpr (P > 0) exchangeC<C>(x, lds, tid, P - 1, P, P - 1, P == NPASS - 1);
+      if constexpr (P > 0)
+        exchangeC<C, P - 1, P, P - 1, P == NPASS - 1, (P >= 2) && wave_local(P - 2, P - 1)>(x, lds, tid);
       fwd_passC<P, C>(x, tw, tid, since_red);
       fwd_fromC<P + 1, C>(x, lds, tw, tid, since_red);
     }
@@ -215,7 +265,8 @@ struct WgNtt {
   __device__ static __forceinline__ void inv_fromC(double (&x)[C][E], double *lds, const double *itw,
                                                    int tid, int &since_red) {
     if constexpr (P >= 0) {
-      if constexpr (P < NPASS - 1) exchangeC<C>(x, lds, tid, P + 1, P, NPASS - 2 - P, P == 0);
+      if constexpr (P < NPASS - 1)
+        exchangeC<C, P + 1, P, NPASS - 2 - P, P == 0, (P + 2 <= NPASS - 1) && wave_local(P + 2, P + 1)>(x, lds, tid);
       inv_passC<P, C>(x, itw, tid, since_red);
       inv_fromC<P - 1, C>(x, lds, itw, tid, since_red);
     }
