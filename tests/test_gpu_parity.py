@@ -182,3 +182,14 @@ def test_end_to_end_gpu_retrieval(real):
     solved = R.decode_payloads(s2, pay, w, D, sorted(found), rp.combination_count)
     for i, p in zip(sorted(found), solved):
         assert p == payloads[i].tolist()
+
+
+def test_native_driver_end_to_end():
+    """The C++ driver (tfhe-omr_amd/examples/omr_e2e.cpp, examples/omr.rs over the C ABI):
+    detect on the GPU, encode both digests, retrieve and check indices and payloads."""
+    import subprocess
+    subprocess.run(["make", "-s", "-C", os.path.join(PL.ROOT, "tfhe-omr_amd"), "examples"], check=True)
+    exe = os.path.join(PL.ROOT, "tfhe-omr_amd", "build", "omr_e2e")
+    r = subprocess.run([exe, "-p", "200"], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "All done: 50 pertinent indices and payloads recovered" in r.stdout

@@ -4,6 +4,7 @@ import os
 import re
 
 import numpy as np
+import pytest
 
 import oracle_lib as O
 import product_lib as PL
@@ -68,3 +69,41 @@ def test_clues_decrypt_to_zero_under_own_key_only():
     # sharding invariance: clue of global index 103 is the same whichever range produced it
     ca2, cb2 = a.gen_clues(5, 103, 2)
     assert np.array_equal(ca2[0], ca[3]) and np.array_equal(cb2[0], cb[3])
+
+
+def _build_e2e():
+    import subprocess
+    subprocess.run(["make", "-s", "-C", os.path.join(PL.ROOT, "tfhe-omr_amd"), "examples"], check=True)
+    return os.path.join(PL.ROOT, "tfhe-omr_amd", "build", "omr_e2e")
+
+
+def test_native_driver_host_only():
+    """examples/omr.rs restated in C++ over include/omr_gpu.h compiles against the header, links
+    the library and runs its CPU part (keys, clues, weights, retrieval parameters)."""
+    import subprocess
+    r = subprocess.run([_build_e2e(), "-p", "300", "--host-only"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert "5 index ct, 28 payload ct" in r.stdout and "host-only: keys, clues" in r.stdout
+
+
+def test_on_disk_formats_round_trip(tmp_path):
+    """OMRF container (omr_amd.write_arrays): keys, clues and ciphertexts round-trip exactly; a
+    wrong kind or a foreign file is rejected."""
+    a, _, dk = PL.keys()
+    p = str(tmp_path / "dk.omrf")
+    A.save_detection_key(p, dk)
+    back = A.load_detection_key(p)
+    for n in ("bsk1", "ksk", "bsk2", "trace_key"):
+        assert np.array_equal(getattr(back, n), getattr(dk, n)) and getattr(back, n).dtype == getattr(dk, n).dtype
+    ca, cb = a.gen_clues(3, 100, 17)
+    A.save_clues(str(tmp_path / "c.omrf"), ca, cb, first=100)
+    la, lb, first = A.load_clues(str(tmp_path / "c.omrf"))
+    assert first == 100 and np.array_equal(la, ca) and np.array_equal(lb, cb)
+    ct = np.random.default_rng(1).integers(0, A.Q2, (3, 2, 2048), dtype=np.uint64)
+    A.save_ciphertexts(str(tmp_path / "ct.omrf"), ct)
+    assert np.array_equal(A.load_ciphertexts(str(tmp_path / "ct.omrf")), ct)
+    with pytest.raises(A.OmrError):
+        A.load_clues(str(tmp_path / "ct.omrf"))
+    (tmp_path / "x.bin").write_bytes(b"not a container")
+    with pytest.raises(A.OmrError):
+        A.load_ciphertexts(str(tmp_path / "x.bin"))

@@ -201,6 +201,83 @@ class SecretKeyPack:
         return a, b
 
 
+# ---- on-disk container (the reference has no serialization) ----------------
+# Little-endian: b"OMRF" | u32 version = 1 | u32 kind | u32 n_arrays | n_arrays x
+# {u32 dtype (1 = u16, 2 = u32, 3 = u64), u32 ndim, u64 dims[4]} | arrays in order, each starting
+# at a 64-byte aligned offset, C order. Kinds: 1 detection key (bsk1, ksk, bsk2, trace_key in the
+# ABI layout of include/omr_gpu.h), 2 clues (clue_a [D][512], clue_b [D][7], first_index [1]),
+# 3 NttRlweCiphertexts (u64 [n][2][2048], e.g. a pertinency vector or a digest).
+_FILE_MAGIC, _FILE_VERSION = b"OMRF", 1
+KIND_DETECTION_KEY, KIND_CLUES, KIND_CIPHERTEXTS = 1, 2, 3
+_DT = {np.dtype(np.uint16): 1, np.dtype(np.uint32): 2, np.dtype(np.uint64): 3}
+_DT_INV = {v: k for k, v in _DT.items()}
+
+
+def write_arrays(path: str, kind: int, arrays) -> None:
+    arrays = [np.ascontiguousarray(a) for a in arrays]
+    head = bytearray(_FILE_MAGIC + np.array([_FILE_VERSION, kind, len(arrays)], "<u4").tobytes())
+    for a in arrays:
+        if a.dtype not in _DT or a.ndim > 4:
+            raise OmrError(f"unsupported array {a.dtype} ndim {a.ndim}")
+        dims = list(a.shape) + [0] * (4 - a.ndim)
+        head += np.array([_DT[a.dtype], a.ndim], "<u4").tobytes() + np.array(dims, "<u8").tobytes()
+    with open(path, "wb") as f:
+        f.write(head)
+        for a in arrays:
+            f.write(b"\0" * (-f.tell() % 64))
+            f.write(a.astype(a.dtype.newbyteorder("<"), copy=False).tobytes())
+
+
+def read_arrays(path: str, kind: int):
+    """Arrays of an OMRF file (memory-mapped, read-only) after checking magic, version and kind."""
+    with open(path, "rb") as f:
+        hdr = f.read(16)
+        if len(hdr) < 16 or hdr[:4] != _FILE_MAGIC:
+            raise OmrError(f"{path}: not an OMRF file")
+        version, k, n = np.frombuffer(hdr[4:16], "<u4")
+        if version != _FILE_VERSION or k != kind:
+            raise OmrError(f"{path}: version {version} kind {k}, expected {_FILE_VERSION} / {kind}")
+        descs = [f.read(40) for _ in range(n)]
+        off = f.tell()
+    out = []
+    for d in descs:
+        dt, nd = np.frombuffer(d[:8], "<u4")
+        shape = tuple(int(x) for x in np.frombuffer(d[8:], "<u8")[:nd])
+        off += -off % 64
+        a = np.memmap(path, dtype=_DT_INV[int(dt)].newbyteorder("<"), mode="r", offset=off, shape=shape)
+        out.append(a)
+        off += a.nbytes
+    return out
+
+
+def save_detection_key(path: str, dk: "DetectionKey") -> None:
+    write_arrays(path, KIND_DETECTION_KEY, [dk.bsk1, dk.ksk, dk.bsk2, dk.trace_key])
+
+
+def load_detection_key(path: str) -> "DetectionKey":
+    b1, k, b2, t = read_arrays(path, KIND_DETECTION_KEY)
+    return DetectionKey(bsk1=np.array(b1), ksk=np.array(k), bsk2=np.array(b2), trace_key=np.array(t))
+
+
+def save_clues(path: str, clue_a, clue_b, first: int = 0) -> None:
+    write_arrays(path, KIND_CLUES, [np.asarray(clue_a, np.uint16), np.asarray(clue_b, np.uint16),
+                                    np.array([first], np.uint64)])
+
+
+def load_clues(path: str):
+    """(clue_a, clue_b, first_index)."""
+    a, b, first = read_arrays(path, KIND_CLUES)
+    return np.array(a), np.array(b), int(first[0])
+
+
+def save_ciphertexts(path: str, cts) -> None:
+    write_arrays(path, KIND_CIPHERTEXTS, [np.asarray(cts, np.uint64).reshape(-1, 2, N2)])
+
+
+def load_ciphertexts(path: str) -> np.ndarray:
+    return np.array(read_arrays(path, KIND_CIPHERTEXTS)[0])
+
+
 def detect_kernels() -> dict:
     """{'br1': name, 'ks': name, 'br2': name} of the kernels this build launches."""
     return dict(kv.split("=") for kv in lib().omr_detect_kernels().decode().split())
