@@ -40,23 +40,19 @@ struct Lvl1Int {
     return x < -H ? x + Q : x;
   }
   __device__ static __forceinline__ uint32_t to_u32(int x) { return (uint32_t)(x < 0 ? x + Q : x); }
-  // NonPowOf2ApproxSignedBasis (logB 5, d 4, drop 7) on a canonical residue: the same digits as
-  // Digits8<LOGB1, D1, DROP1> (floor((v + 2^6) / 2^7), balanced base-32 digits, top unbounded),
-  // packed as signed bytes.
+  // NonPowOf2ApproxSignedBasis (logB 5, d 4, drop 7) on a canonical residue: y = floor((v + 2^6)
+  // / 2^7) has balanced base-32 digits d_k in [-16, 15] (k < 3) and an unbounded top digit; in
+  // closed form, with y' = y + 16 (1 + 32 + 32^2): d_k = ((y' >> 5k) & 31) - 16 for k < 3 and
+  // d_3 = y' >> 15 (the same digits as the recursive Digits8<LOGB1, D1, DROP1>). Returns y'.
+  static constexpr int DIGIT_BIAS = ((1 << (LOGB1 * (D1 - 1))) - 1) / ((1 << LOGB1) - 1) * (1 << (LOGB1 - 1));
   __device__ static __forceinline__ uint32_t digits(int v) {
-    int y = (v + (1 << (DROP1 - 1))) >> DROP1;  // arithmetic shift = floor division
-    uint32_t pk = 0;
-#pragma unroll
-    for (int k = 0; k < D1 - 1; ++k) {
-      const int c = (y + (1 << (LOGB1 - 1))) >> LOGB1;
-      pk |= ((uint32_t)(y - c * (1 << LOGB1)) & 0xffu) << (8 * k);
-      y = c;
-    }
-    return pk | (((uint32_t)y & 0xffu) << (8 * (D1 - 1)));
+    return (uint32_t)(((v + (1 << (DROP1 - 1))) >> DROP1) + DIGIT_BIAS);
   }
-  // signed digit k of a packed word
-  __device__ static __forceinline__ double digit(uint32_t pk, int k) {
-    return (double)((int)(pk << (24 - 8 * k)) >> 24);
+  // signed digit k of y'
+  __device__ static __forceinline__ double digit(uint32_t yb, int k) {
+    const int y = (int)yb;
+    return k < D1 - 1 ? (double)((int)((yb >> (LOGB1 * k)) & ((1u << LOGB1) - 1)) - (1 << (LOGB1 - 1)))
+                      : (double)(y >> (LOGB1 * (D1 - 1)));
   }
   // (X^r * p)[j] for p staged in LDS, r in [0, 2N)
   __device__ static __forceinline__ int rot_read(const int *p, int j, int r) {
