@@ -1,0 +1,60 @@
+"""The closed-form gadget digits used by the kernels (br1_fft.hpp Lvl1Int::digits/digit,
+detect_kernels.hpp Digits2) equal the recursive signed decomposition of the oracle
+(NonPowOf2ApproxSignedBasis: y = floor((v + 2^(drop-1)) / 2^drop), balanced digits, unbounded
+top digit) on boundary and random canonical residues."""
+import numpy as np
+
+import oracle_lib as O
+
+Q1, Q2 = 134215681, 1125899906826241
+
+
+def _recursive(v, logb, d, drop):
+    y = (v + (1 << (drop - 1))) >> drop
+    out = []
+    for _ in range(d - 1):
+        c = (y + (1 << (logb - 1))) >> logb
+        out.append(y - (c << logb))
+        y = c
+    out.append(y)
+    return out
+
+
+def _residues(q, n, seed):
+    h = (q - 1) // 2
+    rng = np.random.default_rng(seed)
+    return np.concatenate([rng.integers(-h, h + 1, n), np.arange(-h, -h + 3000), np.arange(h - 3000, h + 1),
+                           np.arange(-70000, 70000)]).astype(np.int64)
+
+
+def test_level1_closed_form_digits():
+    v = _residues(Q1, 500_000, 1)
+    bias = ((1 << 15) - 1) // 31 * 16  # 16 (1 + 32 + 32^2)
+    yb = (((v + 64) >> 7) + bias).astype(np.int64) & 0xFFFFFFFF  # uint32 word as on the device
+    signed = np.where(yb >= 1 << 31, yb - (1 << 32), yb)
+    closed = [((yb >> (5 * k)) & 31) - 16 for k in range(3)] + [signed >> 15]
+    for a, b in zip(_recursive(v, 5, 4, 7), closed):
+        assert np.array_equal(a, b)
+
+
+def test_level2_closed_form_digits():
+    v = _residues(Q2, 500_000, 2)
+    y = np.floor(v.astype(np.float64) / 256 + 0.5) + 17315143744.0  # exact in FP64 (< 2^42)
+    hi = np.floor(y / 2097152.0)
+    lo = (y - hi * 2097152.0).astype(np.int64)
+    hi = hi.astype(np.int64)
+    closed = [((lo >> (7 * k)) & 127) - 64 for k in range(3)] + [((hi >> (7 * k)) & 127) - 64 for k in range(2)]
+    closed.append(hi >> 14)
+    for a, b in zip(_recursive(v, 7, 6, 8), closed):
+        assert np.array_equal(a, b)
+
+
+def test_recursive_form_is_the_oracle_decomposition():
+    rng = np.random.default_rng(3)
+    for which, q, basis in ((1, Q1, (5, 4, 7)), (2, Q2, (7, 6, 8))):
+        for u in rng.integers(0, q, 300).tolist() + [0, 1, q - 1, (q - 1) // 2, (q + 1) // 2]:
+            c = u - q if u > (q - 1) // 2 else u
+            digits = np.zeros(8, np.int64)
+            n = O.lib().oref_decompose(which, int(u), digits)
+            assert n == basis[1]
+            assert [int(x[0]) for x in _recursive(np.array([c]), *basis)] == digits[:n].tolist()
