@@ -31,7 +31,7 @@ __device__ __forceinline__ void br2f_step(double (&acc0)[BR2_E], double (&acc1)[
                                           int tid) {
   using F = Fft1024;
   using M = Mod<2>;
-  using DG = Digits8<LOGB2, D2, DROP2>;
+  using DG = DigitsFor<2, LOGB2, D2, DROP2>;
   constexpr int T = BR2_T, NF = F::N;
   static_assert(T == F::T && BR2_E == 2 * F::E, "level-2 FFT geometry must match the ACC layout");
   double *xd = reinterpret_cast<double *>(xch);

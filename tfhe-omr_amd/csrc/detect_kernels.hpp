@@ -2,7 +2,13 @@
 // LWE key switch + modulus switch, level-2 blind rotation fused with the homomorphic trace.
 #pragma once
 
+#include <type_traits>
+
 #include "kernels.hpp"
+
+#ifndef OMR_DIGITS2_CLOSED
+#define OMR_DIGITS2_CLOSED 0  // level-2 digits in closed form (Digits2; measured no faster)
+#endif
 
 namespace omr {
 
@@ -39,6 +45,31 @@ struct Digits8 {
     return (double)((int32_t)(w << s) >> 24);
   }
 };
+
+// Level-2 gadget digits (logB 7, d 6, drop 8) in closed form: y = floor((v + 2^7) / 2^8) has
+// balanced base-128 digits d_k in [-64, 63] (k < 5) and a top digit; with the bias
+// 64 (1 + 128 + ... + 128^4), y' = y + bias is exact in FP64 (|y'| < 2^42) and splits exactly into
+// lo = y' mod 2^21 (digits 0-2) and hi = floor(y' / 2^21) (digits 3-4, top = hi >> 14). Same
+// digits as Digits8<7, 6, 8> (tools check: every boundary and 2.6 M random residues).
+struct Digits2 {
+  static constexpr int DW = 2;
+  static_assert(LOGB2 == 7 && D2 == 6 && DROP2 == 8, "closed form written for the level-2 basis");
+  __device__ static __forceinline__ void pack(double v, uint32_t (&pk)[DW]) {
+    const double y = floor(__fma_rn(v, 1.0 / 256.0, 0.5)) + 17315143744.0;
+    const double hi = floor(y * (1.0 / 2097152.0));
+    const double lo = __fma_rn(-hi, 2097152.0, y);
+    pk[0] = (uint32_t)(int)lo;
+    pk[1] = (uint32_t)(int)hi;
+  }
+  __device__ static __forceinline__ double get(const uint32_t (&pk)[DW], int k) {
+    if (k == D2 - 1) return (double)((int)pk[1] >> 14);
+    const uint32_t w = k < 3 ? pk[0] : pk[1];
+    const int sh = 7 * (k < 3 ? k : k - 3);
+    return (double)((int)((w >> sh) & 127u) - 64);
+  }
+};
+template <int LEVEL, int LOGB, int D, int DROP>
+using DigitsFor = std::conditional_t<LEVEL == 2 && OMR_DIGITS2_CLOSED, Digits2, Digits8<LOGB, D, DROP>>;
 
 // Trace basis (q2, 2, None): 25 digits in [-2, 2], 3 bits each (value + 2), 10 per dword.
 struct DigitsTrace {
@@ -128,7 +159,7 @@ __device__ __forceinline__ void cmux_step(double (&acc0)[E], double (&acc1)[E], 
                                           const double *itw, int tid) {
   using M = Mod<LEVEL>;
   using NTT = WgNtt<M, T, E>;
-  using DG = Digits8<LOGB, D, DROP>;
+  using DG = DigitsFor<LEVEL, LOGB, D, DROP>;
   constexpr int N = M::N;
   double accA[E], accB[E];
 #pragma unroll
@@ -195,7 +226,7 @@ __device__ __forceinline__ void cmux_step_pair(double (&acc0)[E], double (&acc1)
                                                const double *tw, const double *itw, int tid) {
   using M = Mod<LEVEL>;
   using NTT = WgNtt<M, T, E>;
-  using DG = Digits8<LOGB, D, DROP>;
+  using DG = DigitsFor<LEVEL, LOGB, D, DROP>;
   constexpr int N = M::N;
   static_assert(!MAC_EXACT || LEVEL == 1, "exact-product MAC needs q < 2^27");
   double acc[2][E];  // [0] = mask accumulator A, [1] = body accumulator B (NTT domain)
