@@ -75,16 +75,18 @@ std::vector<double> negacyclic_lut(const std::vector<uint64_t> &v, int N, int lo
 // the last pass's stages stored lane-minor (WgFft::twiddle_index).
 std::vector<double2> fft_twiddles(int T, int E, int L) {
   const int n = 1 << L, R = __builtin_ctz(E);
+  const int rl = L - ((L + R - 1) / R - 1) * R;  // stages of the last pass
   std::vector<double2> tw(n, make_double2(1.0, 0.0));
   std::vector<int> eps{n};
   for (int s = 0; s < L; ++s) {
     std::vector<int> next;
-    const int k = s - (L - R);  // stage within the last pass (< 0: earlier pass)
+    const int k = s - (L - rl);  // stage within the last pass (< 0: earlier pass)
+    const int q = R - rl + k;    // last pass: node = (lane << q) | j
     for (int i = 0; i < (1 << s); ++i) {
       const int half = eps[i] / 2;
       const long double ang =
           3.14159265358979323846264338327950288L * (long double)half / (long double)(2 * n);
-      const int pos = k < 0 ? (1 << s) + i : (1 << s) + (i & ((1 << k) - 1)) * T + (i >> k);
+      const int pos = k < 0 ? (1 << s) + i : (1 << s) + (i & ((1 << q) - 1)) * T + (i >> q);
       tw[pos] = make_double2((double)cosl(ang), (double)sinl(ang));
       next.push_back(half % (4 * n));
       next.push_back((half + 2 * n) % (4 * n));

@@ -64,6 +64,12 @@ struct FftSwizzle<64, 8, 9> {  // tools/fft_lds_banks.py 64 8 9; tools/fft_lds_p
   static constexpr int PS = 3;
 };
 template <>
+struct FftSwizzle<64, 16, 10> {  // tools/fft_lds_banks.py 64 16 10
+  static constexpr int M[7] = {3, 13, 14, 15, 6, 10, 15};
+  static constexpr bool ADD = false;
+  static constexpr int PS = 0;
+};
+template <>
 struct FftSwizzle<256, 4, 10> {  // tools/fft_lds_banks.py 256 4 10
   static constexpr int M[7] = {2, 13, 6, 0, 4, 4, 2};
   static constexpr bool ADD = false;
@@ -72,13 +78,16 @@ struct FftSwizzle<256, 4, 10> {  // tools/fft_lds_banks.py 256 4 10
 
 template <int T_, int E_, int L_>
 struct WgFft {
-  static constexpr int T = T_, E = E_, L = L_, N = T * E, R = ilog2(E), NPASS = L / R;
-  static_assert(N == (1 << L) && L % R == 0, "FFT geometry");
+  static constexpr int T = T_, E = E_, L = L_, N = T * E, R = ilog2(E), NPASS = (L + R - 1) / R;
+  static_assert(N == (1 << L), "FFT geometry");
+  // stages in pass p (the last pass may be shorter)
+  static constexpr int stages(int p) { return (L - p * R) < R ? (L - p * R) : R; }
 
-  // element index of register e in pass p
+  // element index of register e in pass p (the WgNtt scheme, partial last pass included)
   __device__ static __forceinline__ int index(int p, int lane, int e) {
-    const int lb = L - (p + 1) * R;
-    return ((lane >> lb) << (L - p * R)) | (e << lb) | (lane & ((1 << lb) - 1));
+    const int s0 = p * R, r = stages(p), lb = L - s0 - r;
+    const int F = (lane << (R - r)) | (e >> r);
+    return ((F >> lb) << (L - s0)) | ((e & ((1 << r) - 1)) << lb) | (F & ((1 << lb) - 1));
   }
   // bank-conflict-free XOR swizzle (linear over GF(2); folds to constants per unrolled e)
   template <int... B>
@@ -94,6 +103,7 @@ struct WgFft {
   // slot of register e of `lane` in pass p
   __device__ static __forceinline__ int slot(int p, int lane, int e) {
     if constexpr (ADD) {
+      static_assert(L % R == 0, "additive layout written for full passes");
       const int lb = L - (p + 1) * R;
       const int lp = ((lane >> lb) << (L - p * R)) | (lane & ((1 << lb) - 1));
       const int ep = e << lb;
@@ -107,9 +117,14 @@ struct WgFft {
   // entries; in earlier passes lanes of a group share (broadcast) entries.
   template <int P>
   __device__ static __forceinline__ int twiddle_index(int k, int e, int lane) {
-    constexpr int s0 = P * R, lb = L - s0 - R;
-    if constexpr (P == NPASS - 1) return (1 << (s0 + k)) + (e >> (R - k)) * T + lane;
-    return (1 << (s0 + k)) + (((lane >> lb) << k) | (e >> (R - k)));
+    constexpr int s0 = P * R, r = stages(P), lb = L - s0 - r;
+    const int F = (lane << (R - r)) | (e >> r);
+    const int node = ((F >> lb) << k) | ((e & ((1 << r) - 1)) >> (r - k));
+    if constexpr (P == NPASS - 1) {  // lane-minor: node = (lane << q) | j  ->  (1 << s) + j T + lane
+      const int q = R - r + k;
+      return (1 << (s0 + k)) + (node & ((1 << q) - 1)) * T + lane;
+    }
+    return (1 << (s0 + k)) + node;
   }
 
   template <int C>
@@ -141,7 +156,7 @@ struct WgFft {
   template <int P, bool G>
   __device__ static __forceinline__ double2 twiddle(const double2 *tws, const double2 *__restrict__ gtw,
                                                     int k, int e, int lane) {
-    if constexpr (P == 0 && G) return gtw[(1 << k) + (e >> (R - k))];
+    if constexpr (P == 0 && G) return gtw[(1 << k) + ((e & ((1 << stages(0)) - 1)) >> (stages(0) - k))];
 #ifdef OMR_EXPT_TW_CONST  // timing experiment only (wrong results): no twiddle loads
     return make_double2(0.70710678118654752 + k, 0.70710678118654752 - e);
 #endif
@@ -152,9 +167,10 @@ struct WgFft {
   __device__ static __forceinline__ void fwd_pass(double (&xr)[C][E], double (&xi)[C][E],
                                                   const double2 *tws, int lane,
                                                   const double2 *__restrict__ gtw = nullptr) {
+    constexpr int r = stages(P);
 #pragma unroll
-    for (int k = 0; k < R; ++k) {
-      const int half = 1 << (R - 1 - k);
+    for (int k = 0; k < r; ++k) {
+      const int half = 1 << (r - 1 - k);
 #pragma unroll
       for (int e = 0; e < E; ++e) {
         if (e & half) continue;
@@ -176,9 +192,10 @@ struct WgFft {
   __device__ static __forceinline__ void inv_pass(double (&xr)[C][E], double (&xi)[C][E],
                                                   const double2 *tws, int lane,
                                                   const double2 *__restrict__ gtw = nullptr) {
+    constexpr int r = stages(P);
 #pragma unroll
-    for (int k = R - 1; k >= 0; --k) {
-      const int half = 1 << (R - 1 - k);
+    for (int k = r - 1; k >= 0; --k) {
+      const int half = 1 << (r - 1 - k);
 #pragma unroll
       for (int e = 0; e < E; ++e) {
         if (e & half) continue;
@@ -246,5 +263,6 @@ struct WgFft {
 
 using Fft512 = WgFft<64, 8, 9>;     // level 1: N1 = 1024, one wave
 using Fft1024 = WgFft<256, 4, 10>;  // level 2: N2 = 2048, four waves
+using Fft1024W = WgFft<64, 16, 10>; // level 2: N2 = 2048, one wave (16 points per lane)
 
 }  // namespace omr

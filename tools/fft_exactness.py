@@ -1,109 +1,147 @@
-"""Model of the level-1 wave FFT (tfhe-omr_amd/csrc/device_fft.hpp), lane by lane: checks that
-the twiddle tree, pass indexing and swizzle reproduce the negacyclic product mod X^1024 + 1
-exactly after rounding, and reports the worst rounding error (random and adversarial digits)."""
+"""Lane-exact model of the workgroup FFTs (tfhe-omr_amd/csrc/device_fft.hpp, any T x E, partial
+last pass included): checks that the twiddle tree, pass indexing and swizzle reproduce the
+negacyclic product exactly after rounding, reports the worst rounding error for random and
+adversarial digits, and checks that two geometries of one size agree on the transform order
+(keys transformed by one can be used by the other).
+    python tools/fft_exactness.py            # level 1 (64 x 8, N = 1024)
+    python tools/fft_exactness.py --level 2  # level 2 (256 x 4 and 64 x 16, N = 2048, 2 limbs)"""
+import sys
 import numpy as np
 
-L, R, E, T = 9, 3, 8, 64
-lane = np.arange(T)
 
-def twiddles():
-    eps = {(0, 0): 512}
-    tw = np.zeros(512, dtype=np.complex128)
-    for s in range(9):
-        for i in range(1 << s):
-            e = eps[(s, i)]
-            w_exp = e // 2 if e % 2 == 0 else None
-            assert w_exp is not None
-            tw[(1 << s) + i] = np.exp(1j * np.pi * np.longdouble(w_exp) / 1024)
-            eps[(s + 1, 2 * i)] = (e // 2) % 2048
-            eps[(s + 1, 2 * i + 1)] = (e // 2 + 1024) % 2048
-    return tw
+class Fft:
+    def __init__(self, T, E, L):
+        self.T, self.E, self.L = T, E, L
+        self.R = E.bit_length() - 1
+        self.NP = (L + self.R - 1) // self.R
+        self.n = 1 << L
+        self.lane = np.arange(T)
+        n = self.n
+        eps = {(0, 0): n}
+        self.tw = np.zeros(n, dtype=np.complex128)
+        for s in range(L):
+            for i in range(1 << s):
+                e = eps[(s, i)]
+                self.tw[(1 << s) + i] = np.exp(1j * np.pi * np.longdouble(e // 2) / (2 * n))
+                eps[(s + 1, 2 * i)] = (e // 2) % (4 * n)
+                eps[(s + 1, 2 * i + 1)] = (e // 2 + 2 * n) % (4 * n)
 
-def index(p, e):
-    lb = L - (p + 1) * R
-    return ((lane >> lb) << (L - p * R)) | (e << lb) | (lane & ((1 << lb) - 1))
+    def stages(self, p):
+        return min(self.R, self.L - p * self.R)
 
-def swz(j):
-    return j ^ (((j >> 3) & 1) * 4) ^ (((j >> 4) & 1) * 9) ^ (((j >> 5) & 1) * 15) ^ \
-        (((j >> 6) & 1) * 14) ^ (((j >> 8) & 1) * 8)
+    def index(self, p, e):
+        R, L = self.R, self.L
+        s0, r = p * R, self.stages(p)
+        lb = L - s0 - r
+        F = (self.lane << (R - r)) | (e >> r)
+        return ((F >> lb) << (L - s0)) | ((e & ((1 << r) - 1)) << lb) | (F & ((1 << lb) - 1))
 
-def exchange(x, pf, pt):
-    buf = np.full(512, np.nan, dtype=np.complex128)
-    for e in range(E):
-        buf[swz(index(pf, e))] = x[:, e]
-    assert not np.isnan(buf).any()
-    return np.stack([buf[swz(index(pt, e))] for e in range(E)], axis=1)
+    def node(self, p, k, e):
+        R, L = self.R, self.L
+        s0, r = p * R, self.stages(p)
+        lb = L - s0 - r
+        F = (self.lane << (R - r)) | (e >> r)
+        return (1 << (s0 + k)) + (((F >> lb) << k) | ((e & ((1 << r) - 1)) >> (r - k)))
 
-def fwd_pass(x, P, tw):
-    s0, lb = P * R, L - P * R - R
-    for k in range(R):
-        half = 1 << (R - 1 - k)
-        for e in range(E):
-            if e & half: continue
-            w = tw[(1 << (s0 + k)) + (((lane >> lb) << k) | (e >> (R - k)))]
-            v = x[:, e + half] * w
-            u = x[:, e].copy()
-            x[:, e] = u + v; x[:, e + half] = u - v
-    return x
+    def exchange(self, x, pf, pt):
+        buf = np.full(self.n, np.nan, dtype=np.complex128)
+        for e in range(self.E):
+            buf[self.index(pf, e)] = x[:, e]
+        assert not np.isnan(buf).any()
+        return np.stack([buf[self.index(pt, e)] for e in range(self.E)], axis=1)
 
-def inv_pass(x, P, tw):
-    s0, lb = P * R, L - P * R - R
-    for k in range(R - 1, -1, -1):
-        half = 1 << (R - 1 - k)
-        for e in range(E):
-            if e & half: continue
-            w = tw[(1 << (s0 + k)) + (((lane >> lb) << k) | (e >> (R - k)))]
-            u = x[:, e].copy(); v = x[:, e + half].copy()
-            x[:, e] = u + v; x[:, e + half] = (u - v) * np.conj(w)
-    return x
+    def fwd(self, z):  # z: n complex (folded coefficients) -> x[lane][e] at transform index
+        x = np.stack([z[self.lane + self.T * e] for e in range(self.E)], axis=1).astype(np.complex128)
+        for p in range(self.NP):
+            if p:
+                x = self.exchange(x, p - 1, p)
+            r = self.stages(p)
+            for k in range(r):
+                half = 1 << (r - 1 - k)
+                for e in range(self.E):
+                    if e & half:
+                        continue
+                    w = self.tw[self.node(p, k, e)]
+                    v = x[:, e + half] * w
+                    u = x[:, e].copy()
+                    x[:, e], x[:, e + half] = u + v, u - v
+        out = np.zeros(self.n, dtype=np.complex128)
+        for e in range(self.E):
+            out[self.index(self.NP - 1, e)] = x[:, e]
+        return out  # indexed by transform index
 
-def fwd(p, tw):  # p: real length 1024 -> x[lane][e] at transform index 8 lane + e
-    z = p[:512] + 1j * p[512:]
-    x = np.stack([z[lane + 64 * e] for e in range(E)], axis=1).astype(np.complex128)
-    x = fwd_pass(x, 0, tw); x = exchange(x, 0, 1)
-    x = fwd_pass(x, 1, tw); x = exchange(x, 1, 2)
-    return fwd_pass(x, 2, tw)
+    def inv(self, X):
+        x = np.stack([X[self.index(self.NP - 1, e)] for e in range(self.E)], axis=1).astype(np.complex128)
+        for p in range(self.NP - 1, -1, -1):
+            if p < self.NP - 1:
+                x = self.exchange(x, p + 1, p)
+            r = self.stages(p)
+            for k in range(r - 1, -1, -1):
+                half = 1 << (r - 1 - k)
+                for e in range(self.E):
+                    if e & half:
+                        continue
+                    w = self.tw[self.node(p, k, e)]
+                    u, v = x[:, e].copy(), x[:, e + half].copy()
+                    x[:, e], x[:, e + half] = u + v, (u - v) * np.conj(w)
+        z = np.zeros(self.n, dtype=np.complex128)
+        for e in range(self.E):
+            z[self.lane + self.T * e] = x[:, e]
+        return z
 
-def inv(x, tw):
-    x = inv_pass(x.copy(), 2, tw); x = exchange(x, 2, 1)
-    x = inv_pass(x, 1, tw); x = exchange(x, 1, 0)
-    x = inv_pass(x, 0, tw)
-    z = np.zeros(512, dtype=np.complex128)
-    for e in range(E):
-        z[lane + 64 * e] = x[:, e]
+
+def fold(p):
+    h = len(p) // 2
+    return p[:h] + 1j * p[h:]
+
+
+def unfold(z):
     return np.concatenate([z.real, z.imag])
 
+
 def negacyclic(a, b):
+    N = len(a)
     full = np.convolve(a.astype(object), b.astype(object))
-    r = full[:1024].copy(); r[:1023] -= full[1024:]
+    r = full[:N].copy()
+    r[:N - 1] -= full[N:]
     return r
 
-def main():
-    tw = twiddles()
+
+def adversarial(keys, dmax, N, rng):
+    c = int(rng.integers(N))
+    out = []
+    for k in keys:
+        t = (c - np.arange(N)) % N
+        sign = np.where(np.arange(N) <= c, 1, -1)
+        out.append(dmax * sign * np.sign(k[t]).astype(np.int64))
+    return out
+
+
+def run(geoms, N, kbits, dmax, rows, trials=4):
     rng = np.random.default_rng(5)
-    q1 = 134215681
+    ffts = [Fft(*g) for g in geoms]
     worst = 0.0
-    for trial in range(8):
-        keys = [rng.integers(-(q1 - 1) // 2, (q1 - 1) // 2 + 1, 1024) for _ in range(8)]
-        if trial % 2 == 0:
-            digs = [rng.integers(-16, 18, 1024) for _ in range(8)]
-        else:  # adversarial for output coefficient `c`
-            c = int(rng.integers(1024)); digs = []
-            for k in keys:  # out_c = sum_j d_j * k_{c-j} * sign
-                d = np.zeros(1024, dtype=np.int64)
-                for j in range(1024):
-                    t = c - j; s = 1
-                    if t < 0: t += 1024; s = -1
-                    d[j] = 17 * s * int(np.sign(k[t]))
-                digs.append(d)
-        acc = sum(fwd(d.astype(float), tw) * (fwd(k.astype(float), tw) / 512) for d, k in zip(digs, keys))
-        out = inv(acc, tw)
+    for trial in range(trials):
+        keys = [rng.integers(-(1 << (kbits - 1)), 1 << (kbits - 1), N) for _ in range(rows)]
+        digs = [rng.integers(-dmax, dmax + 1, N) for _ in range(rows)] if trial % 2 == 0 else \
+            adversarial(keys, dmax, N, rng)
         exact = np.array(sum(negacyclic(d, k) for d, k in zip(digs, keys)), dtype=np.float64)
-        err = float(np.max(np.abs(out - exact)))
-        assert np.array_equal(np.rint(out), exact), "rounding mismatch"
-        worst = max(worst, err)
-        print(f"trial {trial}: max |coef| {np.max(np.abs(exact)):.3e}  max error {err:.3e}")
+        spectra = []
+        for f in ffts:
+            acc = sum(f.fwd(fold(d.astype(float))) * (f.fwd(fold(k.astype(float))) / (N // 2))
+                      for d, k in zip(digs, keys))
+            spectra.append(acc)
+            out = unfold(f.inv(acc))
+            assert np.array_equal(np.rint(out), exact), f"rounding mismatch {f.T}x{f.E}"
+            worst = max(worst, float(np.max(np.abs(out - exact))))
+        for a in spectra[1:]:  # same transform order across geometries
+            assert np.allclose(a, spectra[0], rtol=1e-12, atol=1e-6)
+        print(f"trial {trial}: max |coef| {np.max(np.abs(exact)):.3e} worst error so far {worst:.3e}")
     print(f"worst error {worst:.3e} (rounding threshold 0.5)")
 
+
 if __name__ == "__main__":
-    main()
+    if "--level" in sys.argv and sys.argv[sys.argv.index("--level") + 1] == "2":
+        run([(256, 4, 10), (64, 16, 10)], 2048, 25, 64, 12)
+    else:
+        run([(64, 8, 9)], 1024, 27, 17, 8)
