@@ -103,7 +103,7 @@ struct omr_ctx {
   hipStream_t stream = nullptr;
   Key1T *bsk1 = nullptr;    // level-1 NTT-domain keys (OMR_FFT1 == 0)
   double2 *bsk1f = nullptr; // level-1 FFT-domain keys (OMR_FFT1)
-  double2 *fft1 = nullptr, *fft2 = nullptr;
+  double2 *fft1 = nullptr, *fft2 = nullptr, *fft2w = nullptr;
   double2 *bsk2f = nullptr; // level-2 FFT-domain key limbs (OMR_FFT2)
   double *bsk2 = nullptr, *tk = nullptr;
   uint32_t *ksk = nullptr;
@@ -131,7 +131,9 @@ struct omr_ctx {
 #else
 #define OMR_BR1_NAME "br1_kernel"
 #endif
-#if OMR_FFT2
+#if OMR_BR2_SLICED
+#define OMR_BR2_NAME "br2s_trace_kernel"
+#elif OMR_FFT2
 #define OMR_BR2_NAME "br2f_trace_kernel"
 #else
 #define OMR_BR2_NAME "br2_trace_kernel"
@@ -233,7 +235,9 @@ omr_status convert_keys_fft2(const uint64_t *host, size_t npoly, double2 *dev, c
 // Level-2 blind rotation (+ trace, mode 0) of n LWE(670, 4096) ciphertexts.
 omr_status launch_br2(omr_ctx *c, size_t n, const uint32_t *lwe_int, uint64_t *out, int mode,
                       hipStream_t st) {
-#if OMR_FFT2
+#if OMR_BR2_SLICED
+  br2s_trace_kernel<<<(unsigned)n, BR2_T, 0, st>>>(lwe_int, c->bsk2f, c->tk, c->tb, out, mode);
+#elif OMR_FFT2
   br2f_trace_kernel<<<(unsigned)n, BR2_T, 0, st>>>(lwe_int, c->bsk2f, c->tk, c->tb, out, mode);
 #else
   br2_trace_kernel<<<(unsigned)n, BR2_T, 0, st>>>(lwe_int, c->bsk2, c->tk, c->tb, out, mode);
@@ -317,8 +321,13 @@ extern "C" omr_status omr_ctx_create(const omr_detection_key_view *key, int devi
     return fail(set_error(OMR_ERR_OUT_OF_MEMORY, "omr_ctx_create: tables"));
   hipMemcpy(c->fft2, ftw2.data(), ftw2.size() * sizeof(double2), hipMemcpyHostToDevice);
   c->tb.fft2 = c->fft2;
+  const auto ftw2w = fft_twiddles(Fft1024W::T, Fft1024W::E, Fft1024W::L);
+  if (hipMalloc(&c->fft2w, ftw2w.size() * sizeof(double2)) != hipSuccess)
+    return fail(set_error(OMR_ERR_OUT_OF_MEMORY, "omr_ctx_create: tables"));
+  hipMemcpy(c->fft2w, ftw2w.data(), ftw2w.size() * sizeof(double2), hipMemcpyHostToDevice);
+  c->tb.fft2w = c->fft2w;
   // keys
-  const bool fft1 = OMR_FFT1 != 0, fft2 = OMR_FFT2 != 0;
+  const bool fft1 = OMR_FFT1 != 0, fft2 = OMR_FFT2 != 0 || OMR_BR2_SLICED != 0;
   if ((fft1 ? hipMalloc(&c->bsk1f, BSK1_ELEMS / 2 * sizeof(double2))
             : hipMalloc(&c->bsk1, BSK1_ELEMS * sizeof(Key1T))) != hipSuccess ||
       (fft2 ? hipMalloc(&c->bsk2f, BSK2_ELEMS * sizeof(double2))
@@ -355,7 +364,7 @@ extern "C" void omr_ctx_destroy(omr_ctx *c) {
   if (!c) return;
   hipSetDevice(c->device);
   if (c->stream) hipStreamSynchronize(c->stream);
-  for (void *p : {(void *)c->bsk1, (void *)c->bsk1f, (void *)c->fft1, (void *)c->fft2, (void *)c->bsk2f, (void *)c->bsk2, (void *)c->tk, (void *)c->ksk,
+  for (void *p : {(void *)c->bsk1, (void *)c->bsk1f, (void *)c->fft1, (void *)c->fft2, (void *)c->fft2w, (void *)c->bsk2f, (void *)c->bsk2, (void *)c->tk, (void *)c->ksk,
                   (void *)c->tables, (void *)c->trace_tabs, (void *)c->ext, (void *)c->lwe1t,
                   (void *)c->lwe_int, (void *)c->s_clue_a, (void *)c->s_clue_b, (void *)c->s_out,
                   (void *)c->partial})

@@ -590,3 +590,4 @@ __global__ __launch_bounds__(BR2_T, BR2_WAVES) void br2_trace_kernel(const uint3
 }  // namespace omr
 
 #include "br2_fft.hpp"
+#include "br2_sliced.hpp"

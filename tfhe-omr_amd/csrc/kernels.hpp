@@ -48,6 +48,9 @@ namespace omr {
 #define OMR_FFT2 0        // level 2: FP64 complex-FFT external product, 2-limb keys (br2_fft.hpp);
                           // exact and tested, slower than the NTT at this geometry
 #endif
+#ifndef OMR_BR2_SLICED
+#define OMR_BR2_SLICED 0  // level 2: sliced exact-FFT kernel (br2_sliced.hpp); implies FFT-form keys
+#endif
 #ifndef OMR_KEY_NT
 #define OMR_KEY_NT 0
 #endif
@@ -74,7 +77,7 @@ struct DeviceTables {
   const double *lut1, *lut2;              // LUTs, coefficient domain (centred)
   const uint16_t *trace_perm;             // [11][2048] NTT-domain permutation of sigma_g
   const uint16_t *trace_src;              // [11][2048] coefficient source index of sigma_g (+N: negate)
-  const double2 *fft1, *fft2;             // level-1 / level-2 FFT twiddles (device_fft.hpp)
+  const double2 *fft1, *fft2, *fft2w;     // FFT twiddles: level 1, level 2 (256x4), level 2 (64x16)
 };
 
 // ---- key conversion: coefficient-domain canonical residues -> NTT-domain centred residues ----
