@@ -57,7 +57,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--messages", type=int, default=65536, help="clues per GPU")
     ap.add_argument("--pertinent", type=int, default=50)
-    ap.add_argument("--cpu-baseline-msgs", type=int, default=16)
+    ap.add_argument("--cpu-baseline-msgs", type=int, default=256)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-latency", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the encode + reduce + retrieval pass")
@@ -164,10 +164,16 @@ def main():
     dev = torch.device("cuda", local)
     D = args.messages
 
-    # keys + synthetic clues (identical on every rank: seeded, counter-based streams)
+    # keys + synthetic clues (identical on every rank: seeded, counter-based streams), generated on
+    # the GPU (bit-identical to the host generators, tests/test_gpu_parity.py)
     t0 = time.perf_counter()
     pack_a, pack_b = A.SecretKeyPack(42), A.SecretKeyPack(4242)
-    dk = pack_a.generate_detection_key(7)
+    cur = torch.cuda.current_stream(dev).cuda_stream
+    kbufs = [torch.empty(int(np.prod(shape)), dtype=dt, device=dev)
+             for shape, dt in ((A.BSK1_SHAPE, torch.int32), (A.KSK_SHAPE, torch.int32),
+                               (A.BSK2_SHAPE, torch.int64), (A.TK_SHAPE, torch.int64))]
+    pack_a.generate_detection_key_device(7, *[b.data_ptr() for b in kbufs], stream=cur)
+    det = A.Detector.from_device_key(*[b.data_ptr() for b in kbufs], device=local)
     first = rank * D
     total = D * world
     rng = np.random.default_rng(2025)
@@ -175,14 +181,18 @@ def main():
     mask = np.zeros(D, dtype=bool)
     mine = pert[(pert >= first) & (pert < first + D)] - first
     mask[mine] = True
-    ca, cb = pack_a.gen_clues(1000, first, D)
-    na, nb = pack_b.gen_clues(1001, first, D)
-    ca[~mask], cb[~mask] = na[~mask], nb[~mask]
-    det = A.Detector(dk, device=local)
+    d_ca = torch.empty((D, A.N0), dtype=torch.int16, device=dev)
+    d_cb = torch.empty((D, A.CLUE_COUNT), dtype=torch.int16, device=dev)
+    d_na, d_nb = torch.empty_like(d_ca), torch.empty_like(d_cb)
+    pack_a.gen_clues_device(1000, first, D, d_ca.data_ptr(), d_cb.data_ptr(), stream=cur)
+    pack_b.gen_clues_device(1001, first, D, d_na.data_ptr(), d_nb.data_ptr(), stream=cur)
+    d_mask = torch.from_numpy(mask).to(dev)[:, None]
+    d_ca = torch.where(d_mask, d_ca, d_na).contiguous()
+    d_cb = torch.where(d_mask, d_cb, d_nb).contiguous()
+    del d_na, d_nb
+    torch.cuda.synchronize(dev)
     setup_s = time.perf_counter() - t0
 
-    d_ca = torch.from_numpy(ca.view(np.int16)).to(dev)
-    d_cb = torch.from_numpy(cb.view(np.int16)).to(dev)
     d_out = torch.empty((D, 2, 2048), dtype=torch.int64, device=dev)
     stream = torch.cuda.current_stream(dev)
 
@@ -300,7 +310,11 @@ def main():
         "setup_s": round(setup_s, 1),
     }
     if not args.no_cpu_baseline and world == 1:
-        line["cpu_baseline"] = cpu_baseline(dk, ca, cb, args.cpu_baseline_msgs)
+        n = args.cpu_baseline_msgs
+        dk = A.DetectionKey(*[b.cpu().numpy().view(np.uint32 if b.dtype == torch.int32 else np.uint64).reshape(shape)
+                              for b, shape in zip(kbufs, (A.BSK1_SHAPE, A.KSK_SHAPE, A.BSK2_SHAPE, A.TK_SHAPE))])
+        line["cpu_baseline"] = cpu_baseline(dk, d_ca[:n].cpu().numpy().view(np.uint16),
+                                            d_cb[:n].cpu().numpy().view(np.uint16), n)
     print(json.dumps(line), flush=True)
     if dist:
         dist.destroy_process_group()

@@ -85,6 +85,15 @@ omr_status omr_keygen_detection_key(const omr_secret_key_pack *sk, uint64_t seed
  * clue_a u16 [count][512], clue_b u16 [count][7]. */
 omr_status omr_gen_clues(const omr_secret_key_pack *sk, uint64_t seed, uint64_t first,
                          size_t count, uint16_t *clue_a, uint16_t *clue_b, int nthreads);
+/* Device generators: the same streams as omr_gen_clues /
+ * omr_keygen_detection_key, bit-identical output, written to device buffers of the current HIP
+ * device on `stream` (a hipStream_t; NULL = default stream). Both return after the stream has
+ * completed the work. */
+omr_status omr_gen_clues_device(const omr_secret_key_pack *sk, uint64_t seed, uint64_t first,
+                                size_t count, uint16_t *d_clue_a, uint16_t *d_clue_b, void *stream);
+omr_status omr_keygen_detection_key_device(const omr_secret_key_pack *sk, uint64_t seed,
+                                           uint32_t *d_bsk1, uint32_t *d_ksk, uint64_t *d_bsk2,
+                                           uint64_t *d_trace_key, void *stream);
 
 /* ---------------------------------------------------------------------------------------
  * Retrieval layout — RetrievalParams::new(257, 2048, all, pertinent, 130, 25, 2)
@@ -128,7 +137,8 @@ omr_status omr_retrieve_payloads(const omr_secret_key_pack *sk, const uint64_t *
 /* ---------------------------------------------------------------------------------------
  * Detector — one context per GPU; calls on one context are serialised; contexts are
  * independent. Detector::new (detector.rs:85-110) uploads the keys and converts them to the
- * device layout; the LUTs (:457-503) are built inside.
+ * device layout; the LUTs (:457-503) are built inside. The key view may point to host memory
+ * or to device memory of `device` (e.g. from omr_keygen_detection_key_device).
  * ------------------------------------------------------------------------------------- */
 typedef struct omr_ctx omr_ctx;
 

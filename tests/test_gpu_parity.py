@@ -193,3 +193,43 @@ def test_native_driver_end_to_end():
     r = subprocess.run([exe, "-p", "200"], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "All done: 50 pertinent indices and payloads recovered" in r.stdout
+
+
+def _dev_u(n, itemsize):
+    import torch
+    return torch.empty(n, dtype={2: torch.int16, 4: torch.int32, 8: torch.int64}[itemsize], device="cuda:0")
+
+
+def _host(t, dtype):
+    return t.cpu().numpy().view(dtype)
+
+
+def test_gpu_clue_generation_matches_host():
+    """omr_gen_clues_device == the host generator, bit for bit, for both packs,
+    at an offset global index (stream id = global message index)."""
+    a_sk, b_sk, _ = PL.keys()
+    for sk, seed, first, count in ((a_sk, 1000, 0, 257), (b_sk, 1001, 123456, 1000)):
+        ha, hb = sk.gen_clues(seed, first, count)
+        da, db = _dev_u(count * A.N0, 2), _dev_u(count * A.CLUE_COUNT, 2)
+        sk.gen_clues_device(seed, first, count, da.data_ptr(), db.data_ptr())
+        assert np.array_equal(_host(da, np.uint16).reshape(ha.shape), ha)
+        assert np.array_equal(_host(db, np.uint16).reshape(hb.shape), hb)
+
+
+def test_gpu_keygen_matches_host_and_detects():
+    """omr_keygen_detection_key_device == the host key generator, bit for bit
+    (all four components, including rejection-sampled rows), and a Detector built straight
+    from the device-resident key gives the same detect output as one built from host keys."""
+    a_sk, b_sk, dk = PL.keys()
+    parts = [(dk.bsk1, 4), (dk.ksk, 4), (dk.bsk2, 8), (dk.trace_key, 8)]
+    bufs = [_dev_u(h.size, it) for h, it in parts]
+    a_sk.generate_detection_key_device(PL.KEY_SEED, *[b.data_ptr() for b in bufs])
+    for (h, _), b in zip(parts, bufs):
+        assert np.array_equal(_host(b, h.dtype).reshape(h.shape), h)
+    mask = np.zeros(6, bool)
+    mask[[1, 4]] = True
+    ca, cb = PL.mixed_clues(mask, seed=77)
+    want = A.Detector(dk).detect_batch(ca, cb)
+    det = A.Detector.from_device_key(*[b.data_ptr() for b in bufs])
+    del bufs  # the context holds its own converted copy
+    assert np.array_equal(det.detect_batch(ca, cb), want)

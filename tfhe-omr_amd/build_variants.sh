@@ -3,7 +3,7 @@
 set -e
 mk() { name=$1; shift
   mkdir -p build/var_$name
-  for s in keygen context retriever; do
+  for s in keygen keygen_gpu context retriever; do
     /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -ffp-contract=off -I../include "$@" -c csrc/$s.hip -o build/var_$name/$s.o &
   done; wait
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o build/var_$name.so build/var_$name/*.o -lpthread

@@ -175,7 +175,7 @@ omr_status convert_keys(const IN *host, size_t npoly, OUT *dev, double scale, co
   HIP_TRY(hipMalloc(&tmp, chunk * N * sizeof(IN)));
   for (size_t p0 = 0; p0 < npoly; p0 += chunk) {
     const size_t n = std::min(chunk, npoly - p0);
-    HIP_TRY(hipMemcpyAsync(tmp, host + p0 * N, n * N * sizeof(IN), hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(tmp, host + p0 * N, n * N * sizeof(IN), hipMemcpyDefault, st));
     key_to_ntt_kernel<LEVEL, IN, OUT><<<n, T, 0, st>>>(tmp, dev + p0 * N, n, scale, tw);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(st));
@@ -191,7 +191,7 @@ omr_status convert_keys_fft1(const uint32_t *host, size_t npoly, double2 *dev, c
   HIP_TRY(hipMalloc(&tmp, chunk * N1 * sizeof(uint32_t)));
   for (size_t p0 = 0; p0 < npoly; p0 += chunk) {
     const size_t n = std::min(chunk, npoly - p0);
-    HIP_TRY(hipMemcpyAsync(tmp, host + p0 * N1, n * N1 * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(tmp, host + p0 * N1, n * N1 * sizeof(uint32_t), hipMemcpyDefault, st));
     key_to_fft1_kernel<<<n, 64, 0, st>>>(tmp, dev + p0 * Fft512::N, n, tw);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(st));
@@ -223,7 +223,7 @@ omr_status convert_keys_fft2(const uint64_t *host, size_t npoly, double2 *dev, c
   HIP_TRY(hipMalloc(&tmp, chunk * N2 * sizeof(uint64_t)));
   for (size_t p0 = 0; p0 < npoly; p0 += chunk) {
     const size_t n = std::min(chunk, npoly - p0);
-    HIP_TRY(hipMemcpyAsync(tmp, host + p0 * N2, n * N2 * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(tmp, host + p0 * N2, n * N2 * sizeof(uint64_t), hipMemcpyDefault, st));
     key_to_fft2_kernel<<<n, 256, 0, st>>>(tmp, dev + p0 * 2 * Fft1024::N, n, tw);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(st));
@@ -350,7 +350,7 @@ extern "C" omr_status omr_ctx_create(const omr_detection_key_view *key, int devi
                                       c->stream)) != OMR_OK)
     return fail(st);
   scale_even_rows_kernel<<<(TK_ELEMS / N2 + 1) / 2, 256, 0, c->stream>>>(c->tk, TK_ELEMS / N2, ninv2);
-  if (hipMemcpyAsync(c->ksk, key->ksk, KSK_ELEMS * sizeof(uint32_t), hipMemcpyHostToDevice,
+  if (hipMemcpyAsync(c->ksk, key->ksk, KSK_ELEMS * sizeof(uint32_t), hipMemcpyDefault,
                      c->stream) != hipSuccess ||
       hipMemsetAsync(c->ksk + KSK_ELEMS, 0, 64 * sizeof(uint32_t), c->stream) != hipSuccess ||
       hipStreamSynchronize(c->stream) != hipSuccess)

@@ -34,10 +34,11 @@
 
 namespace omr {
 
-// LDS visibility within one wave: wait for this wave's LDS operations and keep the compiler
-// from moving memory operations across (waves of a workgroup stay independent).
+// LDS visibility within one wave: keep the compiler from moving memory operations across (waves
+// of a workgroup stay independent). One wave's LDS instructions execute in issue order, so the
+// lgkmcnt wait is only needed with OMR_WAVE_SYNC_WAIT (the conservative form).
 __device__ __forceinline__ void wave_lds_sync() {
-  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+  if (OMR_WAVE_SYNC_WAIT) __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
   __builtin_amdgcn_wave_barrier();
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
 }

@@ -13,6 +13,9 @@
 #ifndef OMR_NTT_WAVE_LOCAL
 #define OMR_NTT_WAVE_LOCAL 1  // wave-level sync for NTT exchanges that stay inside each wave
 #endif
+#ifndef OMR_WAVE_SYNC_WAIT
+#define OMR_WAVE_SYNC_WAIT 1  // wave-local exchanges wait for the wave's own LDS writes
+#endif
 #ifndef OMR_DB_XCH
 #define OMR_DB_XCH 1  // NTT exchanges through two alternating LDS buffers (fewer barriers)
 #endif
@@ -138,7 +141,7 @@ struct WgNtt {
     return true;
   }
   __device__ static __forceinline__ void wave_sync() {
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+    if (OMR_WAVE_SYNC_WAIT) __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0), see wave_lds_sync
     __builtin_amdgcn_wave_barrier();
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
   }

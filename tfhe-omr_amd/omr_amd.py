@@ -59,6 +59,10 @@ EXPORTS = {
     "omr_secret_export": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "omr_keygen_detection_key": (C.c_int, [C.c_void_p, C.c_uint64, _u32p, _u32p, _u64p, _u64p, C.c_int]),
     "omr_gen_clues": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64, C.c_size_t, _u16p, _u16p, C.c_int]),
+    "omr_gen_clues_device": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64, C.c_size_t, C.c_void_p, C.c_void_p,
+                                       C.c_void_p]),
+    "omr_keygen_detection_key_device": (C.c_int, [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p,
+                                                  C.c_void_p, C.c_void_p]),
     "omr_get_retrieval_params": (C.c_int, [C.c_size_t, C.c_size_t, C.POINTER(_RetrievalParams)]),
     "omr_payload_weights": (C.c_int, [_u8p, C.c_size_t, C.c_uint32, C.c_uint32, C.c_uint32, _u16p]),
     "omr_ctx_create": (C.c_int, [C.POINTER(_KeyView), C.c_int, C.POINTER(C.c_void_p)]),
@@ -200,6 +204,17 @@ class SecretKeyPack:
                "omr_gen_clues")
         return a, b
 
+    # Device generators: same streams, bit-identical results, written to
+    # device buffers (ABI layout) of the current HIP device; return when the stream is done.
+    def gen_clues_device(self, seed: int, first: int, count: int, d_clue_a: int, d_clue_b: int, stream: int = 0):
+        _check(lib().omr_gen_clues_device(self._h, seed, first, count, d_clue_a, d_clue_b, stream or None),
+               "omr_gen_clues_device")
+
+    def generate_detection_key_device(self, seed: int, d_bsk1: int, d_ksk: int, d_bsk2: int, d_trace_key: int,
+                                      stream: int = 0):
+        _check(lib().omr_keygen_detection_key_device(self._h, seed, d_bsk1, d_ksk, d_bsk2, d_trace_key,
+                                                     stream or None), "omr_keygen_detection_key_device")
+
 
 # ---- on-disk container (the reference has no serialization) ----------------
 # Little-endian: b"OMRF" | u32 version = 1 | u32 kind | u32 n_arrays | n_arrays x
@@ -339,6 +354,18 @@ class Detector:
         _check(lib().omr_ctx_create(C.byref(view), device, C.byref(h)), "omr_ctx_create")
         self._h = h
         self.device = device
+
+    @classmethod
+    def from_device_key(cls, d_bsk1: int, d_ksk: int, d_bsk2: int, d_trace_key: int, device: int = 0):
+        """Detector over key components already in the HBM of `device` (device pointers, ABI
+        layout), e.g. from SecretKeyPack.generate_detection_key_device."""
+        self = cls.__new__(cls)
+        view = _KeyView(d_bsk1, d_ksk, d_bsk2, d_trace_key)
+        h = C.c_void_p()
+        _check(lib().omr_ctx_create(C.byref(view), device, C.byref(h)), "omr_ctx_create")
+        self._h = h
+        self.device = device
+        return self
 
     def close(self):
         if getattr(self, "_h", None):
