@@ -58,6 +58,8 @@ def parse():
     ap.add_argument("--messages", type=int, default=65536, help="clues per GPU")
     ap.add_argument("--pertinent", type=int, default=50)
     ap.add_argument("--cpu-baseline-msgs", type=int, default=256)
+    ap.add_argument("--force-dist", action="store_true",
+                    help="initialise the RCCL process group even at world size 1 (rehearses the N > 1 path)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-latency", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the encode + reduce + retrieval pass")
@@ -153,7 +155,7 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    if world > 1 or args.force_dist:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
@@ -280,7 +282,7 @@ def main():
                    "frac": round(lane_instr / FP64_PEAK_T_LANE_INSTR, 4), "tflops": round(flops, 2),
                    "counts_from": comp.get("source")}
     line = {
-        "metric": "detect-phase messages/sec (D=65536 per GPU)",
+        "metric": "detect-phase messages/sec + per-message latency, D=65536 at 1/2/4/8 MI355X",
         "value": round(value, 2),
         "unit": "messages/s",
         "n_gpus": world,

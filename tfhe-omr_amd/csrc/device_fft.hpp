@@ -34,6 +34,10 @@
 
 namespace omr {
 
+#ifndef OMR_FFT_DB
+#define OMR_FFT_DB 1  // multi-wave FFTs: double-buffered, wave-local where the pass pair allows
+#endif
+
 // LDS visibility within one wave: keep the compiler from moving memory operations across (waves
 // of a workgroup stay independent). One wave's LDS instructions execute in issue order, so the
 // lgkmcnt wait is only needed with OMR_WAVE_SYNC_WAIT (the conservative form).
@@ -128,27 +132,61 @@ struct WgFft {
     return (1 << (s0 + k)) + node;
   }
 
-  template <int C>
+  // lane owning element idx in pass p (inverse of index())
+  static constexpr int thread_of(int p, int idx) {
+    const int s0 = p * R, r = stages(p), lb = L - s0 - r;
+    const int F = ((idx >> (L - s0)) << lb) | (idx & ((1 << lb) - 1));
+    return F >> (R - r);
+  }
+  // every element stays in its wave between passes pf and pt (the swizzle keeps the bits above
+  // the low four, so each wave then reads and writes only its own slots)
+  static constexpr bool wave_local(int pf, int pt) {
+    if (T <= 64) return true;
+    for (int idx = 0; idx < N; ++idx)
+      if ((thread_of(pf, idx) >> 6) != (thread_of(pt, idx) >> 6)) return false;
+    return true;
+  }
+  // Multi-wave single transforms alternate two LDS buffers (lds then holds 2 * BUF): only the
+  // transform's last exchange needs a barrier after its reads.
+  static constexpr bool DB = T > 64 && OMR_FFT_DB != 0;
+
+  // Exchange PF -> PT, the ORD-th of the transform. LAST: no exchange of this transform follows.
+  // PREV_WL: the previous exchange was wave-local (other waves may still read their slots).
+  template <int C, int PF, int PT, int ORD, bool LAST, bool PREV_WL>
   __device__ static __forceinline__ void exchange(double (&xr)[C][E], double (&xi)[C][E],
-                                                  double2 *lds, int lane, int p_from, int p_to) {
+                                                  double2 *lds, int lane) {
 #ifdef OMR_EXPT_NO_EXCH  // timing experiment only (wrong results): no LDS exchange
     return;
 #endif
+    constexpr bool WL = wave_local(PF, PT);
+    constexpr bool db = DB && C == 1;
+    if constexpr (T > 64 && !WL && PREV_WL) __syncthreads();
+    double2 *buf = lds + (db ? (ORD & 1) * BUF : 0);
 #pragma unroll
     for (int c = 0; c < C; ++c)
 #pragma unroll
       for (int e = 0; e < E; ++e)
-        lds[c * BUF + slot(p_from, lane, e)] = make_double2(xr[c][e], xi[c][e]);
-    fft_sync<T>();
+        buf[c * BUF + slot(PF, lane, e)] = make_double2(xr[c][e], xi[c][e]);
+    if constexpr (WL)
+      wave_lds_sync();
+    else
+      __syncthreads();
 #pragma unroll
     for (int c = 0; c < C; ++c)
 #pragma unroll
       for (int e = 0; e < E; ++e) {
-        const double2 v = lds[c * BUF + slot(p_to, lane, e)];
+        const double2 v = buf[c * BUF + slot(PT, lane, e)];
         xr[c][e] = v.x;
         xi[c][e] = v.y;
       }
-    fft_sync<T>();
+    if constexpr (T <= 64) {
+      wave_lds_sync();
+    } else if constexpr (LAST || !db) {
+      if constexpr (!LAST && WL)
+        wave_lds_sync();
+      else
+        __syncthreads();
+    }
   }
 
   // Pass 0's node index does not depend on the lane (lane >> (L - R) == 0), so its twiddles
@@ -222,10 +260,12 @@ struct WgFft {
                                              const double2 *__restrict__ gtw = nullptr) {
     static_assert(NPASS <= 5, "unrolled for up to 5 passes");
     fwd_pass<0, C, G>(xr, xi, tws, lane, gtw);
-#define OMR_FFT_FWD_STEP(P)                            \
-  if constexpr (NPASS > P) {                           \
-    exchange<C>(xr, xi, lds, lane, P - 1, P);          \
-    fwd_pass<(NPASS > P ? P : 0), C>(xr, xi, tws, lane); \
+#define OMR_FFT_FWD_STEP(P)                                                                   \
+  if constexpr (NPASS > P) {                                                                  \
+    constexpr int Q = NPASS > P ? P : 1;                                                      \
+    exchange<C, Q - 1, Q, Q - 1, Q == NPASS - 1, (Q >= 2) && wave_local(Q >= 2 ? Q - 2 : 0, Q - 1)>( \
+        xr, xi, lds, lane);                                                                   \
+    fwd_pass<(NPASS > P ? P : 0), C>(xr, xi, tws, lane);                                      \
   }
     OMR_FFT_FWD_STEP(1)
     OMR_FFT_FWD_STEP(2)
@@ -238,10 +278,12 @@ struct WgFft {
                                              const double2 *tws, int lane,
                                              const double2 *__restrict__ gtw = nullptr) {
     static_assert(NPASS <= 5, "unrolled for up to 5 passes");
-#define OMR_FFT_INV_STEP(P)                            \
-  if constexpr (NPASS > P) {                           \
-    inv_pass<(NPASS > P ? P : 0), C>(xr, xi, tws, lane); \
-    exchange<C>(xr, xi, lds, lane, P, P - 1);          \
+#define OMR_FFT_INV_STEP(P)                                                                   \
+  if constexpr (NPASS > P) {                                                                  \
+    constexpr int Q = NPASS > P ? P : 1;                                                      \
+    inv_pass<(NPASS > P ? P : 0), C>(xr, xi, tws, lane);                                      \
+    exchange<C, Q, Q - 1, NPASS - 1 - Q, Q == 1,                                              \
+             (Q + 1 <= NPASS - 1) && wave_local(Q + 1 <= NPASS - 1 ? Q + 1 : Q, Q)>(xr, xi, lds, lane); \
   }
     OMR_FFT_INV_STEP(4)
     OMR_FFT_INV_STEP(3)
