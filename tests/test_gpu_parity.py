@@ -233,3 +233,29 @@ def test_gpu_keygen_matches_host_and_detects():
     det = A.Detector.from_device_key(*[b.data_ptr() for b in bufs])
     del bufs  # the context holds its own converted copy
     assert np.array_equal(det.detect_batch(ca, cb), want)
+
+
+def test_edge_inputs_bit_exact(real):
+    """Inputs the KATs never produce, bit-exact against the oracle: all-zero clues (every CMUX
+    step has a_i = 0), all-maximal clues (a_i = 2047), uniformly random clue words (not
+    encryptions), and a ragged batch split into chunks of 5 (12 = 5 + 5 + 2, and 7 rotations per
+    message so the level-1 workgroups of 4 rotations straddle messages). D = 0 is a no-op."""
+    _, det, orc = real
+    rng = np.random.default_rng(99)
+    cases = [
+        (np.zeros((2, A.N0), np.uint16), np.zeros((2, A.CLUE_COUNT), np.uint16)),
+        (np.full((2, A.N0), 2047, np.uint16), np.full((2, A.CLUE_COUNT), 2047, np.uint16)),
+        (rng.integers(0, 2048, (3, A.N0)).astype(np.uint16), rng.integers(0, 2048, (3, A.CLUE_COUNT)).astype(np.uint16)),
+    ]
+    for ca, cb in cases:
+        assert np.array_equal(det.detect_batch(ca, cb), orc.detect_batch(ca, cb))
+    mask = rng.random(12) < 0.5
+    ca, cb = PL.mixed_clues(mask, seed=4321, first=1000)
+    det.set_batch(5)
+    try:
+        got = det.detect_batch(ca, cb)
+    finally:
+        det.set_batch(0)
+    assert np.array_equal(got, orc.detect_batch(ca, cb))
+    empty = det.detect_batch(np.zeros((0, A.N0), np.uint16), np.zeros((0, A.CLUE_COUNT), np.uint16))
+    assert empty.shape == (0, 2, A.N2)

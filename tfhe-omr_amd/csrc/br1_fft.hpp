@@ -29,6 +29,10 @@ namespace omr {
 #ifndef BR1F_RW
 #define BR1F_RW 1  // level-1 rotations per wave (key rows shared, transforms interleaved)
 #endif
+#ifndef BR1F_BARRIERS
+#define BR1F_BARRIERS 2  // workgroup barriers per staged key row (1: next row issued after the MAC barrier;
+                         // exposes the row latency: 212 vs 199 ms at D = 4,096)
+#endif
 #ifndef BR1F_KEY_SPLIT
 #define BR1F_KEY_SPLIT 1  // load the B component of a key row after the transform (32 VGPRs less)
 #endif
@@ -213,9 +217,11 @@ __device__ __forceinline__ void br1f_step_lds(int (&ac)[2][16], double2 *xch, co
 #pragma unroll 1
     for (int k = 0; k < D1; ++k) {
       const int q = q0 + p * D1 + k;
-      wg_barrier_lds();  // every wave has finished reading buffer (q + 1) & 1 (row q - 1)
       const bool more = q + 1 < qtotal;
+#if BR1F_BARRIERS == 2
+      wg_barrier_lds();  // every wave has finished reading buffer (q + 1) & 1 (row q - 1)
       if (more) krow_issue(bskf + (size_t)(q + 1) * KROW_SLOTS, kbuf + ((q + 1) & 1) * KROW_SLOTS, lane, wave);
+#endif
       double xr[8], xi[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
@@ -223,11 +229,17 @@ __device__ __forceinline__ void br1f_step_lds(int (&ac)[2][16], double2 *xch, co
         xi[e] = Lvl1Int::digit(pk[p][8 + e], k);
       }
       F::fwd(xr, xi, xch, tws, lane);
+#if BR1F_BARRIERS == 2
       if (more)
         vm_wait_row_in_flight();  // row q landed (row q + 1 may stay in flight)
       else
         vm_wait_all();
       wg_barrier_lds();  // ... in every wave's share
+#else
+      vm_wait_all();     // this wave's share of row q landed (the only copy in flight)
+      wg_barrier_lds();  // row q complete, and every wave is done with row q - 1 (its buffer)
+      if (more) krow_issue(bskf + (size_t)(q + 1) * KROW_SLOTS, kbuf + ((q + 1) & 1) * KROW_SLOTS, lane, wave);
+#endif
       const double2 *kb = kbuf + (q & 1) * KROW_SLOTS;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
