@@ -29,6 +29,9 @@ namespace omr {
 #ifndef BR1F_RW
 #define BR1F_RW 1  // level-1 rotations per wave (key rows shared, transforms interleaved)
 #endif
+#ifndef BR1F_GTW
+#define BR1F_GTW 1  // pass-0 twiddles (wave-uniform) by scalar loads from the global table (-2.6 %)
+#endif
 #ifndef BR1F_BARRIERS
 #define BR1F_BARRIERS 2  // workgroup barriers per staged key row (1: next row issued after the MAC barrier;
                          // exposes the row latency: 212 vs 199 ms at D = 4,096)
@@ -203,8 +206,10 @@ __device__ __forceinline__ void wg_barrier_lds() {  // LDS reads/writes done, th
 // consumed, row q0+8 (next step's first) is prefetched at the end. kbuf: 2 staged rows.
 __device__ __forceinline__ void br1f_step_lds(int (&ac)[2][16], double2 *xch, const double2 *tws,
                                               int a, const double2 *__restrict__ bskf, int q0,
-                                              int qtotal, double2 *kbuf, int lane, int wave) {
+                                              int qtotal, double2 *kbuf, int lane, int wave,
+                                              const double2 *__restrict__ gtw) {
   using F = Fft512;
+  using X = double(&)[1][8];
   uint32_t pk[2][16];
   br1f_digits(ac, reinterpret_cast<int *>(xch), a, lane, pk);
   double outr[2][8], outi[2][8];
@@ -228,7 +233,7 @@ __device__ __forceinline__ void br1f_step_lds(int (&ac)[2][16], double2 *xch, co
         xr[e] = Lvl1Int::digit(pk[p][e], k);
         xi[e] = Lvl1Int::digit(pk[p][8 + e], k);
       }
-      F::fwd(xr, xi, xch, tws, lane);
+      F::fwd<1, BR1F_GTW != 0>(reinterpret_cast<X>(xr), reinterpret_cast<X>(xi), xch, tws, lane, gtw);
 #if BR1F_BARRIERS == 2
       if (more)
         vm_wait_row_in_flight();  // row q landed (row q + 1 may stay in flight)
@@ -253,7 +258,7 @@ __device__ __forceinline__ void br1f_step_lds(int (&ac)[2][16], double2 *xch, co
   }
 #pragma unroll
   for (int o = 0; o < 2; ++o) {
-    F::inv(outr[o], outi[o], xch, tws, lane);
+    F::inv<1, BR1F_GTW != 0>(reinterpret_cast<X>(outr[o]), reinterpret_cast<X>(outi[o]), xch, tws, lane, gtw);
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const double v = rint(i < 8 ? outr[o][i] : outi[o][i - 8]);  // exact (< 2^43)
@@ -323,7 +328,7 @@ __global__ __launch_bounds__(64 * BR1F_WPG, BR1F_WAVES) void br1f_kernel(
   for (int i = 0; i < N0; ++i) {
     int a[RW];
     a[0] = __builtin_amdgcn_readfirstlane(la[0][i]);
-    br1f_step_lds(ac[0], xch, tws, a[0], bskf, i * 2 * D1, N0 * 2 * D1, kbuf, lane, wave);
+    br1f_step_lds(ac[0], xch, tws, a[0], bskf, i * 2 * D1, N0 * 2 * D1, kbuf, lane, wave, tb.fft1);
   }
   __syncthreads();
 #else

@@ -34,6 +34,9 @@
 
 namespace omr {
 
+#ifndef OMR_FFT_TW_PAIR
+#define OMR_FFT_TW_PAIR 1  // odd sibling nodes reuse the even node's twiddle (w_odd = i w_even)
+#endif
 #ifndef OMR_FFT_DB
 #define OMR_FFT_DB 1  // multi-wave FFTs: double-buffered, wave-local where the pass pair allows
 #endif
@@ -213,16 +216,21 @@ struct WgFft {
 #pragma unroll
       for (int e = 0; e < E; ++e) {
         if (e & half) continue;
-        const double2 w = twiddle<P, G>(tws, gtw, k, e, lane);
+        // sibling nodes 2j, 2j + 1 have twiddles w and i w (half-angles of eps and eps + 2n):
+        // odd nodes reuse the even twiddle and apply the factor i by swapping parts (fewer LDS
+        // twiddle reads, no extra arithmetic)
+        const int pb = (OMR_FFT_TW_PAIR && k >= 1) ? (1 << (r - k)) : 0;
+        const bool odd = (e & pb) != 0;
+        const double2 w = twiddle<P, G>(tws, gtw, k, odd ? (e & ~pb) : e, lane);
 #pragma unroll
         for (int c = 0; c < C; ++c) {
           const double vr = __fma_rn(xr[c][e + half], w.x, -xi[c][e + half] * w.y);
           const double vi = __fma_rn(xr[c][e + half], w.y, xi[c][e + half] * w.x);
           const double ur = xr[c][e], ui = xi[c][e];
-          xr[c][e] = ur + vr;
-          xi[c][e] = ui + vi;
-          xr[c][e + half] = ur - vr;
-          xi[c][e + half] = ui - vi;
+          xr[c][e] = odd ? ur - vi : ur + vr;  // u + i v  |  u + v
+          xi[c][e] = odd ? ui + vr : ui + vi;
+          xr[c][e + half] = odd ? ur + vi : ur - vr;
+          xi[c][e + half] = odd ? ui - vr : ui - vi;
         }
       }
     }
@@ -238,16 +246,19 @@ struct WgFft {
 #pragma unroll
       for (int e = 0; e < E; ++e) {
         if (e & half) continue;
-        const double2 w = twiddle<P, G>(tws, gtw, k, e, lane);
+        const int pb = (OMR_FFT_TW_PAIR && k >= 1) ? (1 << (r - k)) : 0;  // see fwd_pass
+        const bool odd = (e & pb) != 0;
+        const double2 w = twiddle<P, G>(tws, gtw, k, odd ? (e & ~pb) : e, lane);
 #pragma unroll
         for (int c = 0; c < C; ++c) {
           const double ur = xr[c][e], ui = xi[c][e];
           const double dr = ur - xr[c][e + half], di = ui - xi[c][e + half];
           xr[c][e] = ur + xr[c][e + half];
           xi[c][e] = ui + xi[c][e + half];
-          // (dr + i di) * conj(w)
-          xr[c][e + half] = __fma_rn(dr, w.x, di * w.y);
-          xi[c][e + half] = __fma_rn(di, w.x, -dr * w.y);
+          // (dr + i di) * conj(w); odd node: conj(i w) = -i conj(w)
+          const double tr = __fma_rn(dr, w.x, di * w.y), ti = __fma_rn(di, w.x, -dr * w.y);
+          xr[c][e + half] = odd ? ti : tr;
+          xi[c][e + half] = odd ? -tr : ti;
         }
       }
     }

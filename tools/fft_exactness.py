@@ -10,8 +10,8 @@ import numpy as np
 
 
 class Fft:
-    def __init__(self, T, E, L):
-        self.T, self.E, self.L = T, E, L
+    def __init__(self, T, E, L, pair=True):
+        self.T, self.E, self.L, self.pair = T, E, L, pair
         self.R = E.bit_length() - 1
         self.NP = (L + self.R - 1) // self.R
         self.n = 1 << L
@@ -43,6 +43,15 @@ class Fft:
         F = (self.lane << (R - r)) | (e >> r)
         return (1 << (s0 + k)) + (((F >> lb) << k) | ((e & ((1 << r) - 1)) >> (r - k)))
 
+    def twiddle(self, p, k, e):
+        """(w, odd): with pairing (OMR_FFT_TW_PAIR) an odd sibling node reads its even sibling's
+        twiddle and the kernel applies the factor i (w_odd = i w_even)."""
+        r = self.stages(p)
+        pb = (1 << (r - k)) if (self.pair and k >= 1) else 0
+        odd = bool(e & pb)
+        w = self.tw[self.node(p, k, e & ~pb if odd else e)]
+        return w, odd
+
     def exchange(self, x, pf, pt):
         buf = np.full(self.n, np.nan, dtype=np.complex128)
         for e in range(self.E):
@@ -61,8 +70,8 @@ class Fft:
                 for e in range(self.E):
                     if e & half:
                         continue
-                    w = self.tw[self.node(p, k, e)]
-                    v = x[:, e + half] * w
+                    w, odd = self.twiddle(p, k, e)
+                    v = x[:, e + half] * w * (1j if odd else 1)
                     u = x[:, e].copy()
                     x[:, e], x[:, e + half] = u + v, u - v
         out = np.zeros(self.n, dtype=np.complex128)
@@ -81,9 +90,9 @@ class Fft:
                 for e in range(self.E):
                     if e & half:
                         continue
-                    w = self.tw[self.node(p, k, e)]
+                    w, odd = self.twiddle(p, k, e)
                     u, v = x[:, e].copy(), x[:, e + half].copy()
-                    x[:, e], x[:, e + half] = u + v, (u - v) * np.conj(w)
+                    x[:, e], x[:, e + half] = u + v, (u - v) * np.conj(w) * (-1j if odd else 1)
         z = np.zeros(self.n, dtype=np.complex128)
         for e in range(self.E):
             z[self.lane + self.T * e] = x[:, e]
