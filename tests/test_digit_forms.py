@@ -35,6 +35,19 @@ def test_level1_closed_form_digits():
     closed = [((yb >> (5 * k)) & 31) - 16 for k in range(3)] + [signed >> 15]
     for a, b in zip(_recursive(v, 5, 4, 7), closed):
         assert np.array_equal(a, b)
+    # the word the kernel keeps (Lvl1Int::digits): yb ^ bias, each digit one signed bit-field
+    # of width 5 at offset 5k (k < 3) or 17 at offset 15 (top digit); the kernel extracts it with
+    # two uniform shifts, (int)(w << (32 - off - width)) >> (32 - width)
+    w = yb ^ bias
+    ws = np.where(w >= 1 << 31, w - (1 << 32), w)
+
+    def sbfe(x, off, width):
+        f = (x >> off) & ((1 << width) - 1)
+        return np.where(f >= 1 << (width - 1), f - (1 << width), f)
+
+    extracted = [sbfe(w, 5 * k, 5) for k in range(3)] + [sbfe(ws & 0xFFFFFFFF, 15, 17)]
+    for a, b in zip(_recursive(v, 5, 4, 7), extracted):
+        assert np.array_equal(a, b)
 
 
 def test_level2_closed_form_digits():

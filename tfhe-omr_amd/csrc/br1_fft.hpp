@@ -36,6 +36,12 @@ namespace omr {
 #define BR1F_BARRIERS 2  // workgroup barriers per staged key row (1: next row issued after the MAC barrier;
                          // exposes the row latency: 212 vs 199 ms at D = 4,096)
 #endif
+#ifndef BR1F_DIGIT_SBFE
+#define BR1F_DIGIT_SBFE 2  // digit words in two's-complement fields; 2: two uniform shifts per digit, 1: v_bfe_i32 (inline asm, slower)
+#endif
+#ifndef BR1F_ROT_EXT
+#define BR1F_ROT_EXT 1  // rotation through a negacyclic extension [ACC, -ACC] per poly
+#endif
 #ifndef BR1F_KEY_SPLIT
 #define BR1F_KEY_SPLIT 1  // load the B component of a key row after the transform (32 VGPRs less)
 #endif
@@ -50,16 +56,14 @@ struct Lvl1Int {
   // NonPowOf2ApproxSignedBasis (logB 5, d 4, drop 7) on a canonical residue: y = floor((v + 2^6)
   // / 2^7) has balanced base-32 digits d_k in [-16, 15] (k < 3) and an unbounded top digit; in
   // closed form, with y' = y + 16 (1 + 32 + 32^2): d_k = ((y' >> 5k) & 31) - 16 for k < 3 and
-  // d_3 = y' >> 15 (the same digits as the recursive Digits8<LOGB1, D1, DROP1>). Returns y'.
+  // d_3 = y' >> 15 (the same digits as the recursive Digits8<LOGB1, D1, DROP1>). The word kept is
+  // y' ^ (16 (1 + 32 + 32^2)): field k then holds d_k in two's complement (d_k + 16 = f in
+  // [0, 32) and (f - 16) mod 32 = f ^ 16), the top digit is unchanged, and every digit is one
+  // signed bit-field extract with wave-uniform offset and width (digit()). Returns that word.
   static constexpr int DIGIT_BIAS = ((1 << (LOGB1 * (D1 - 1))) - 1) / ((1 << LOGB1) - 1) * (1 << (LOGB1 - 1));
   __device__ static __forceinline__ uint32_t digits(int v) {
-    return (uint32_t)(((v + (1 << (DROP1 - 1))) >> DROP1) + DIGIT_BIAS);
-  }
-  // signed digit k of y'
-  __device__ static __forceinline__ double digit(uint32_t yb, int k) {
-    const int y = (int)yb;
-    return k < D1 - 1 ? (double)((int)((yb >> (LOGB1 * k)) & ((1u << LOGB1) - 1)) - (1 << (LOGB1 - 1)))
-                      : (double)(y >> (LOGB1 * (D1 - 1)));
+    return (uint32_t)(((v + (1 << (DROP1 - 1))) >> DROP1) + DIGIT_BIAS) ^
+           (BR1F_DIGIT_SBFE ? (uint32_t)DIGIT_BIAS : 0u);
   }
   // (X^r * p)[j] for p staged in LDS, r in [0, 2N)
   __device__ static __forceinline__ int rot_read(const int *p, int j, int r) {
@@ -70,26 +74,62 @@ struct Lvl1Int {
     const int v = p[u];
     return neg ? -v : v;
   }
+  // signed digit k of a digits() word
+  __device__ static __forceinline__ double digit(uint32_t w, int k) {
+    if (!BR1F_DIGIT_SBFE)
+      return k < D1 - 1 ? (double)((int)((w >> (LOGB1 * k)) & ((1u << LOGB1) - 1)) - (1 << (LOGB1 - 1)))
+                        : (double)((int)w >> (LOGB1 * (D1 - 1)));
+    if (BR1F_DIGIT_SBFE == 2) {  // two uniform shifts: field to the top, arithmetic shift down
+      const int s1 = k < D1 - 1 ? 32 - LOGB1 * (k + 1) : 0, s2 = k < D1 - 1 ? 32 - LOGB1 : LOGB1 * (D1 - 1);
+      return (double)((int)(w << s1) >> s2);
+    }
+    const int off = LOGB1 * k, width = k < D1 - 1 ? LOGB1 : 32 - LOGB1 * (D1 - 1);
+    // v_bfe_i32 by inline asm: clang turns (double)__builtin_amdgcn_sbfe(x, off, width) with a
+    // non-constant width into v_cvt_f64_u32 (wrong for negative digits; ROCm 7.2)
+    int d;
+    asm("v_bfe_i32 %0, %1, %2, %3" : "=v"(d) : "v"(w), "s"(off), "v"(width));
+    return (double)d;
+  }
 };
 
 // ACC layout: ac[p][h * 8 + e] = coefficient lane + 64 e + 512 h of poly p (0 mask, 1 body).
 __device__ __forceinline__ int acc_coef(int lane, int i) { return lane + 64 * (i & 7) + 512 * (i >> 3); }
 
-// digits of (X^a - 1) * ACC for both polys (ACC staged through the LDS buffer st, 8 KB)
+// digits of (X^a - 1) * ACC for both polys. Each poly is staged with its negacyclic extension
+// ext = [ACC, -ACC] (2N int32 = the wave's 8 KB buffer st), so (X^a * ACC)[j] = ext[(j - a) mod 2N]:
+// one masked index and no sign fix-up per coefficient.
 __device__ __forceinline__ void br1f_digits(const int (&ac)[2][16], int *st, int a, int lane,
                                             uint32_t (&pk)[2][16]) {
+  if (!BR1F_ROT_EXT) {  // both polys staged at once (8 KB), sign-corrected rotated reads
 #pragma unroll
-  for (int p = 0; p < 2; ++p)
+    for (int p = 0; p < 2; ++p)
 #pragma unroll
-    for (int i = 0; i < 16; ++i) st[p * N1 + acc_coef(lane, i)] = ac[p][i];
-  wave_lds_sync();
+      for (int i = 0; i < 16; ++i) st[p * N1 + acc_coef(lane, i)] = ac[p][i];
+    wave_lds_sync();
 #pragma unroll
-  for (int p = 0; p < 2; ++p)
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+      for (int i = 0; i < 16; ++i)
+        pk[p][i] = Lvl1Int::digits(
+            Lvl1Int::canon(Lvl1Int::rot_read(st + p * N1, acc_coef(lane, i), a) - ac[p][i]));
+    wave_lds_sync();
+    return;
+  }
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      st[acc_coef(lane, i)] = ac[p][i];
+      st[N1 + acc_coef(lane, i)] = -ac[p][i];
+    }
+    wave_lds_sync();
+    const int base = lane - a + 2 * N1;
 #pragma unroll
     for (int i = 0; i < 16; ++i)
       pk[p][i] = Lvl1Int::digits(
-          Lvl1Int::canon(Lvl1Int::rot_read(st + p * N1, acc_coef(lane, i), a) - ac[p][i]));
-  wave_lds_sync();
+          Lvl1Int::canon(st[(base + acc_coef(0, i)) & (2 * N1 - 1)] - ac[p][i]));
+    wave_lds_sync();
+  }
 }
 
 // One CMUX step for RW rotations held by this wave (all at the same key row i; a[r] may be 0,

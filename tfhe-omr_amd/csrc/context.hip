@@ -237,10 +237,30 @@ omr_status launch_br2(omr_ctx *c, size_t n, const uint32_t *lwe_int, uint64_t *o
                       hipStream_t st) {
 #if OMR_BR2_SLICED
   br2s_trace_kernel<<<(unsigned)n, BR2_T, 0, st>>>(lwe_int, c->bsk2f, c->tk, c->tb, out, mode);
-#elif OMR_FFT2
-  br2f_trace_kernel<<<(unsigned)n, BR2_T, 0, st>>>(lwe_int, c->bsk2f, c->tk, c->tb, out, mode);
 #else
-  br2_trace_kernel<<<(unsigned)n, BR2_T, 0, st>>>(lwe_int, c->bsk2, c->tk, c->tb, out, mode);
+#if OMR_FFT2
+  auto kern = br2f_trace_kernel;
+  const auto *keys = c->bsk2f;
+#else
+  auto kern = br2_trace_kernel;
+  const auto *keys = c->bsk2;
+#endif
+  size_t gen = n;
+  if (OMR_BR2_PERSIST) {
+    // Launch in generations of one resident grid each: the workgroups of a generation start
+    // together and do the same work, so they stay near the same CMUX step and share each key
+    // row through L2, instead of drifting over the whole key as replacement workgroups would.
+    int dev = 0, cus = 0, per_cu = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, BR2_T, 0));
+    gen = std::max<size_t>(1, (size_t)cus * (size_t)(per_cu > 0 ? per_cu : 1));
+  }
+  for (size_t off = 0; off < n; off += gen) {
+    const size_t m = std::min(gen, n - off);
+    kern<<<(unsigned)m, BR2_T, 0, st>>>(lwe_int + off * (NI + 1), keys, c->tk, c->tb,
+                                        out + off * 2 * N2, mode);
+  }
 #endif
   HIP_TRY(hipGetLastError());
   return OMR_OK;

@@ -153,10 +153,12 @@ __device__ __forceinline__ void rotate_diff(const double (&src)[E], double *xch,
   __syncthreads();
 }
 
-template <int LEVEL, int T, int E, int LOGB, int D, int DROP, typename KeyT, int DEPTH>
+template <int LEVEL, int T, int E, int LOGB, int D, int DROP, typename KeyT, int DEPTH, bool G = false>
 __device__ __forceinline__ void cmux_step(double (&acc0)[E], double (&acc1)[E], double *xch, int a,
                                           const KeyT *__restrict__ ggsw, const double *tw,
-                                          const double *itw, int tid) {
+                                          const double *itw, int tid,
+                                          const double *__restrict__ gtw = nullptr,
+                                          const double *__restrict__ gitw = nullptr) {
   using M = Mod<LEVEL>;
   using NTT = WgNtt<M, T, E>;
   using DG = DigitsFor<LEVEL, LOGB, D, DROP>;
@@ -182,7 +184,10 @@ __device__ __forceinline__ void cmux_step(double (&acc0)[E], double (&acc1)[E], 
     double x[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) x[e] = DG::get(pk[e], k);
-    NTT::fwd(x, xch, tw, tid);
+    if constexpr (G)
+      NTT::fwd_g(x, xch, tw, gtw, tid);
+    else
+      NTT::fwd(x, xch, tw, tid);
 #pragma unroll
     for (int e = 0; e < E; ++e) {
       accA[e] += mm<M>(x[e], (double)cur.a[e]);
@@ -207,10 +212,16 @@ __device__ __forceinline__ void cmux_step(double (&acc0)[E], double (&acc1)[E], 
     accA[e] = red<M>(accA[e]);
     accB[e] = red<M>(accB[e]);
   }
-  NTT::inv(accA, xch, itw, tid);
+  if constexpr (G)
+    NTT::inv_g(accA, xch, itw, gitw, tid);
+  else
+    NTT::inv(accA, xch, itw, tid);
 #pragma unroll
   for (int e = 0; e < E; ++e) acc0[e] = canon<M>(acc0[e] + accA[e]);
-  NTT::inv(accB, xch, itw, tid);
+  if constexpr (G)
+    NTT::inv_g(accB, xch, itw, gitw, tid);
+  else
+    NTT::inv(accB, xch, itw, tid);
 #pragma unroll
   for (int e = 0; e < E; ++e) acc1[e] = canon<M>(acc1[e] + accB[e]);
 }
@@ -571,8 +582,9 @@ __global__ __launch_bounds__(BR2_T, BR2_WAVES) void br2_trace_kernel(const uint3
     cmux_step_pair<2, T, E, LOGB2, D2, DROP2, Key2T, OMR_KEY_DEPTH2, false>(
         acc0, acc1, xch, a, bsk2 + (size_t)OMR_KEYROW2(i) * (2 * D2 * 2 * N), tw, itw, tid);
 #else
-    cmux_step<2, T, E, LOGB2, D2, DROP2, Key2T, OMR_KEY_DEPTH2>(
-        acc0, acc1, xch, a, bsk2 + (size_t)OMR_KEYROW2(i) * (2 * D2 * 2 * N), tw, itw, tid);
+    cmux_step<2, T, E, LOGB2, D2, DROP2, Key2T, OMR_KEY_DEPTH2, OMR_NTT_GTW != 0>(
+        acc0, acc1, xch, a, bsk2 + (size_t)OMR_KEYROW2(i) * (2 * D2 * 2 * N), tw, itw, tid, tb.tw2,
+        tb.itw2);
 #endif
   }
   uint64_t *o = out + wg * 2 * N;

@@ -178,9 +178,10 @@ struct WgNtt {
     }
   }
 
-  template <int P, int C>
+  // G: pass 0's twiddles (wave-uniform: hi == 0) come from the global table gtw by scalar loads
+  template <int P, int C, bool G = false>
   __device__ static __forceinline__ void fwd_passC(double (&x)[C][E], const double *tw, int tid,
-                                                   int &since_red) {
+                                                   int &since_red, const double *__restrict__ gtw = nullptr) {
     constexpr int s0 = P * R;
     constexpr int r = (L - s0) < R ? (L - s0) : R;
     constexpr int lb = L - s0 - r;
@@ -202,7 +203,8 @@ struct WgNtt {
 #ifdef OMR_EXPT_NTT_TW_CONST  // timing experiment only (wrong results)
         const double w = 1234567.0 + s * 3 + e;
 #else
-        const double w = tw[(1 << s) + ((hi << k) | (ep >> (r - k)))];
+        const double w = (P == 0 && G) ? gtw[(1 << s) + (ep >> (r - k))]
+                                       : tw[(1 << s) + ((hi << k) | (ep >> (r - k)))];
 #endif
 #pragma unroll
         for (int c = 0; c < C; ++c) {
@@ -216,9 +218,9 @@ struct WgNtt {
     }
   }
 
-  template <int P, int C>
+  template <int P, int C, bool G = false>
   __device__ static __forceinline__ void inv_passC(double (&x)[C][E], const double *itw, int tid,
-                                                   int &since_red) {
+                                                   int &since_red, const double *__restrict__ gitw = nullptr) {
     constexpr int s0 = P * R;
     constexpr int r = (L - s0) < R ? (L - s0) : R;
     constexpr int lb = L - s0 - r;
@@ -240,7 +242,8 @@ struct WgNtt {
 #ifdef OMR_EXPT_NTT_TW_CONST  // timing experiment only (wrong results)
         const double w = 7654321.0 + s * 3 + e;
 #else
-        const double w = itw[(1 << s) + ((hi << k) | (ep >> (r - k)))];
+        const double w = (P == 0 && G) ? gitw[(1 << s) + (ep >> (r - k))]
+                                       : itw[(1 << s) + ((hi << k) | (ep >> (r - k)))];
 #endif
 #pragma unroll
         for (int c = 0; c < C; ++c) {
@@ -254,24 +257,26 @@ struct WgNtt {
     }
   }
 
-  template <int P, int C>
+  template <int P, int C, bool G = false>
   __device__ static __forceinline__ void fwd_fromC(double (&x)[C][E], double *lds, const double *tw,
-                                                   int tid, int &since_red) {
+                                                   int tid, int &since_red,
+                                                   const double *__restrict__ gtw = nullptr) {
     if constexpr (P < NPASS) {
       if constexpr (P > 0)
         exchangeC<C, P - 1, P, P - 1, P == NPASS - 1, (P >= 2) && wave_local(P - 2, P - 1)>(x, lds, tid);
-      fwd_passC<P, C>(x, tw, tid, since_red);
-      fwd_fromC<P + 1, C>(x, lds, tw, tid, since_red);
+      fwd_passC<P, C, G>(x, tw, tid, since_red, gtw);
+      fwd_fromC<P + 1, C, G>(x, lds, tw, tid, since_red, gtw);
     }
   }
-  template <int P, int C>
+  template <int P, int C, bool G = false>
   __device__ static __forceinline__ void inv_fromC(double (&x)[C][E], double *lds, const double *itw,
-                                                   int tid, int &since_red) {
+                                                   int tid, int &since_red,
+                                                   const double *__restrict__ gitw = nullptr) {
     if constexpr (P >= 0) {
       if constexpr (P < NPASS - 1)
         exchangeC<C, P + 1, P, NPASS - 2 - P, P == 0, (P + 2 <= NPASS - 1) && wave_local(P + 2, P + 1)>(x, lds, tid);
-      inv_passC<P, C>(x, itw, tid, since_red);
-      inv_fromC<P - 1, C>(x, lds, itw, tid, since_red);
+      inv_passC<P, C, G>(x, itw, tid, since_red, gitw);
+      inv_fromC<P - 1, C, G>(x, lds, itw, tid, since_red, gitw);
     }
   }
 
@@ -287,6 +292,21 @@ struct WgNtt {
                                               int tid) {
     int since_red = 0;
     inv_fromC<NPASS - 1, C>(x, lds, itw, tid, since_red);
+  }
+
+  // Single transforms with pass 0's twiddles from the global tables (scalar loads): pass 0 has
+  // hi == 0 for every thread (T = 2^(L - R)), so its 2^R - 1 twiddles are workgroup-uniform.
+  __device__ static __forceinline__ void fwd_g(double (&x)[E], double *lds, const double *tw,
+                                               const double *__restrict__ gtw, int tid) {
+    static_assert(T == (1 << (L - R)), "pass-0 twiddles uniform only for a full first pass");
+    int since_red = 0;
+    fwd_fromC<0, 1, true>(reinterpret_cast<double(&)[1][E]>(x), lds, tw, tid, since_red, gtw);
+  }
+  __device__ static __forceinline__ void inv_g(double (&x)[E], double *lds, const double *itw,
+                                               const double *__restrict__ gitw, int tid) {
+    static_assert(T == (1 << (L - R)), "pass-0 twiddles uniform only for a full first pass");
+    int since_red = 0;
+    inv_fromC<NPASS - 1, 1, true>(reinterpret_cast<double(&)[1][E]>(x), lds, itw, tid, since_red, gitw);
   }
 
   // Single-transform API.

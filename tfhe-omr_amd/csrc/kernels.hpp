@@ -51,6 +51,12 @@ namespace omr {
 #ifndef OMR_BR2_SLICED
 #define OMR_BR2_SLICED 0  // level 2: sliced exact-FFT kernel (br2_sliced.hpp); implies FFT-form keys
 #endif
+#ifndef OMR_NTT_GTW
+#define OMR_NTT_GTW 0     // level 2: pass-0 NTT twiddles (workgroup-uniform) by scalar loads (+1.5 %: off)
+#endif
+#ifndef OMR_BR2_PERSIST
+#define OMR_BR2_PERSIST 0 // level 2: resident-sized grid walking messages with a grid stride
+#endif
 #ifndef OMR_KEY_NT
 #define OMR_KEY_NT 0
 #endif
