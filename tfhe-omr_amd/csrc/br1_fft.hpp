@@ -42,6 +42,9 @@ namespace omr {
 #ifndef BR1F_ROT_EXT
 #define BR1F_ROT_EXT 1  // rotation through a negacyclic extension [ACC, -ACC] per poly
 #endif
+#ifndef BR1F_CANON_MIN
+#define BR1F_CANON_MIN 1  // level-1 int canonicalisation by unsigned min folds (no VCC hazards)
+#endif
 #ifndef BR1F_KEY_SPLIT
 #define BR1F_KEY_SPLIT 1  // load the B component of a key row after the transform (32 VGPRs less)
 #endif
@@ -49,8 +52,17 @@ namespace omr {
 struct Lvl1Int {
   static constexpr int Q = 134215681, H = 67107840;
   __device__ static __forceinline__ int canon(int x) {  // |x| < q + H -> [-H, H]
-    x = x > H ? x - Q : x;
-    return x < -H ? x + Q : x;
+    if (!BR1F_CANON_MIN) {
+      x = x > H ? x - Q : x;
+      return x < -H ? x + Q : x;
+    }
+    // unsigned min folds, no VCC (compare/select pairs serialise on VCC with hazard NOPs):
+    // y = x + H in [-Q, 2Q); min(y, y + Q) lifts [-Q, 0) into [0, Q), min(y, y - Q) lowers
+    // [Q, 2Q) into [0, Q) (the other operand wraps above 2^31 and loses)
+    uint32_t y = (uint32_t)(x + H);
+    y = min(y, y + (uint32_t)Q);
+    y = min(y, y - (uint32_t)Q);
+    return (int)y - H;
   }
   __device__ static __forceinline__ uint32_t to_u32(int x) { return (uint32_t)(x < 0 ? x + Q : x); }
   // NonPowOf2ApproxSignedBasis (logB 5, d 4, drop 7) on a canonical residue: y = floor((v + 2^6)

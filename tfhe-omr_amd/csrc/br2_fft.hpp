@@ -26,6 +26,7 @@ namespace omr {
 
 constexpr double LIMB2 = 33554432.0;  // 2^25
 
+#ifdef OMR_BR2_GEOM_DEFAULT
 __device__ __forceinline__ void br2f_step(double (&acc0)[BR2_E], double (&acc1)[BR2_E], double2 *xch,
                                           const double2 *tws, int a, const double2 *__restrict__ ggsw,
                                           int tid) {
@@ -204,6 +205,8 @@ __global__ __launch_bounds__(BR2_T, BR2_WAVES) void br2f_trace_kernel(
   __syncthreads();
   hom_trace_store(acc0, acc1, reinterpret_cast<double *>(xch), tabs, tabs + N, tk, tb, o, tid);
 }
+
+#endif  // OMR_BR2_GEOM_DEFAULT
 
 // Coefficient-domain canonical u64 key polynomials -> two 25-bit limbs, each FFT-transformed and
 // scaled by 1/1024, stored [poly][limb][1024] complex in transform-index order.

@@ -31,6 +31,7 @@ __device__ __forceinline__ int slot_swz(int t) {
          (((t >> 7) & 1) * 13) ^ (((t >> 9) & 1) * 1);
 }
 
+#ifdef OMR_BR2_GEOM_DEFAULT
 __global__ __launch_bounds__(256, 1) void br2s_trace_kernel(const uint32_t *__restrict__ lwe_int,
                                                             const double2 *__restrict__ bskf,
                                                             const double *__restrict__ tk,
@@ -191,5 +192,7 @@ __global__ __launch_bounds__(256, 1) void br2s_trace_kernel(const uint32_t *__re
   __syncthreads();
   hom_trace_store(acc0, acc1, xd, tabs, tabs + N, tk, tb, o, tid);
 }
+
+#endif  // OMR_BR2_GEOM_DEFAULT
 
 }  // namespace omr

@@ -16,6 +16,9 @@
 #ifndef OMR_WAVE_SYNC_WAIT
 #define OMR_WAVE_SYNC_WAIT 1  // wave-local exchanges wait for the wave's own LDS writes
 #endif
+#ifndef OMR_CANON_RED
+#define OMR_CANON_RED 1  // canonical residues by a second rounded reduction (no VCC selects)
+#endif
 #ifndef OMR_DB_XCH
 #define OMR_DB_XCH 1  // NTT exchanges through two alternating LDS buffers (fewer barriers)
 #endif
@@ -55,10 +58,16 @@ template <class M>
 __device__ __forceinline__ double red(double x) {
   return __fma_rn(-rint(x * M::QINV), M::Q, x);
 }
+// For an integer |x| <= q - 1, red(x) is already the exact centred representative: fl(x / q)
+// errs by far less than the 2^-52 gap between (q +- 1) / 2q and 1/2, so rint picks the right
+// quotient at the +-(q-1)/2 boundaries (checked for both primes). red(red(x)) therefore
+// canonicalises any |x| < 2^53 (red leaves |r| <= q/2 + 2) without compare/select pairs, which
+// serialise on VCC with hazard NOPs (OMR_CANON_RED = 0 keeps the select form).
 // exact centred representative in [-(q-1)/2, (q-1)/2]
 template <class M>
 __device__ __forceinline__ double canon(double x) {
   double r = red<M>(x);
+  if (OMR_CANON_RED) return red<M>(r);
   r = r > M::HALF ? r - M::Q : r;
   r = r < -M::HALF ? r + M::Q : r;
   return r;
@@ -66,6 +75,7 @@ __device__ __forceinline__ double canon(double x) {
 // for |x| <= q - 1 (sum/difference of two canonical values)
 template <class M>
 __device__ __forceinline__ double canon_small(double x) {
+  if (OMR_CANON_RED) return red<M>(x);
   x = x > M::HALF ? x - M::Q : x;
   x = x < -M::HALF ? x + M::Q : x;
   return x;

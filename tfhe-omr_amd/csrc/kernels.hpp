@@ -20,6 +20,7 @@ namespace omr {
 #endif
 #ifndef BR2_TE
 #define BR2_TE 256, 8
+#define OMR_BR2_GEOM_DEFAULT 1  // the level-2 FFT / sliced options are written for 256 x 8
 #endif
 #ifndef OMR_KEY_DEPTH1
 #define OMR_KEY_DEPTH1 1  // level-1 key rows prefetched this many digits ahead (1 or 2)
