@@ -84,6 +84,17 @@ def cpu_baseline(dk, ca, cb, nmsg):
             "sample": f"{nmsg} detect() calls of the same workload, OpenMP over messages, {dt:.1f}s wall"}
 
 
+def workload_name(D, world):
+    """BASELINE.json config the run corresponds to (configs[2] at D = 65,536 per GPU, configs[3]
+    at N = 8, configs[4]'s detect + encode shape at D = 2^20 over the job)."""
+    name = f"full detect() D={D} per GPU, {D * world} total"
+    if D == 65536:
+        name += " (configs[2]; configs[3] at N=8)"
+    elif D * world == 1 << 20:
+        name += " (configs[4]: detect + encode + retrieval at D=2^20)"
+    return name
+
+
 def load_profile(name):
     """A committed rocprofv3 summary under profiles/ (tools/profile.sh, tools/compute_summary.py)."""
     path = os.path.join(ROOT, "profiles", name)
@@ -212,11 +223,12 @@ def main():
     torch.cuda.synchronize(dev)
     t = time.perf_counter()
     start.record(stream)
-    for _ in range(args.steps):
+    for i in range(args.steps):
         step()
-        info = det.last_timing()  # per-stage HIP events recorded on `stream`
+        info = det.last_timing()  # per-stage HIP events recorded on `stream` (waits for them)
         for k in stage:
             stage[k] += info[k]
+        print(f"[bench] rank {rank} step {i + 1}/{args.steps} done", file=sys.stderr, flush=True)
     end.record(stream)
     torch.cuda.synchronize(dev)
     if dist:
@@ -295,7 +307,7 @@ def main():
         "vs_baseline_ref": "published 1-thread AVX-512 CPU detect, 234.07 ms/msg (README.md:122)",
         "dtype": "f64",
         "data": "synthetic (seeded keys and clues; 50 pertinent over the whole job)",
-        "config": {"workload": "full detect() D=65536 per GPU (configs[2]; configs[3] at N=8)",
+        "config": {"workload": workload_name(D, world),
                    "messages_per_gpu": D, "messages_total": D * world,
                    "pertinent": int(len(pert)), "batch": 16384, "parallelism": f"dp{world}"},
         "latency_ms_per_message": latency_ms,

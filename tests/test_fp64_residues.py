@@ -1,0 +1,62 @@
+"""The FP64 residue canonicalisation the kernels use (device_ntt.hpp canon / canon_small with
+OMR_CANON_RED, br1_fft.hpp Lvl1Int::canon with BR1F_CANON_MIN), replayed in numpy with the
+device's IEEE operations: red(x) = x - rint(x * fl(1/q)) * q (the product q * rint(...) and the
+difference are exact in FP64 here, as the device's fma is), rint = round half to even.
+
+Claims checked at both primes:
+  * red(x) is the exact centred representative for every integer |x| <= q - 1 (sums and
+    differences of two canonical residues), including the +-(q-1)/2, +-(q+1)/2 boundaries;
+  * red(red(x)) is the exact centred representative for integers |x| < 2^53.
+and the int32 unsigned-min fold of the level-1 accumulator update."""
+import numpy as np
+
+Q1, Q2 = 134215681, 1125899906826241
+
+
+def _red(x, q):
+    x = np.asarray(x, dtype=np.float64)
+    qinv = np.float64(1.0) / np.float64(q)
+    return x - np.rint(x * qinv) * np.float64(q)
+
+
+def _centred(x, q):
+    r = np.mod(x, q)
+    return np.where(r > (q - 1) // 2, r - q, r)
+
+
+def test_red_canonicalises_sums_of_canonical_residues():
+    rng = np.random.default_rng(11)
+    for q in (Q1, Q2):
+        h = (q - 1) // 2
+        xs = np.concatenate([np.arange(h - 20000, h + 20001), np.arange(-h - 20000, -h + 20001),
+                             np.arange(q - 20000, q), np.arange(-q + 1, -q + 20001),
+                             rng.integers(-(q - 1), q, 400_000)]).astype(np.int64)
+        xs = xs[np.abs(xs) <= q - 1]
+        got = _red(xs.astype(np.float64), q)
+        assert np.array_equal(got.astype(np.int64), _centred(xs, q))
+        assert np.all(np.abs(got) <= h)
+
+
+def test_double_red_canonicalises_below_2_53():
+    rng = np.random.default_rng(12)
+    for q in (Q1, Q2):
+        xs = rng.integers(-(1 << 53) + 1, 1 << 53, 400_000, dtype=np.int64)
+        # values next to multiples of q plus/minus half: where a single rint can land one off
+        k = rng.integers(-(1 << 53) // q + 1, (1 << 53) // q - 1, 50_000, dtype=np.int64)
+        edge = np.concatenate([k * q + (q - 1) // 2 + d for d in (-2, -1, 0, 1, 2, 3)])
+        xs = np.concatenate([xs, edge])
+        got = _red(_red(xs.astype(np.float64), q), q)
+        assert np.array_equal(got.astype(np.int64), _centred(xs, q))
+
+
+def test_level1_unsigned_min_canon():
+    q, h = Q1, (Q1 - 1) // 2
+    rng = np.random.default_rng(13)
+    x = np.concatenate([rng.integers(-q - h + 1, q + h, 400_000), np.arange(-q - h + 1, -q - h + 2000),
+                        np.arange(q + h - 2000, q + h), np.arange(-h - 2000, -h + 2000),
+                        np.arange(h - 2000, h + 2000)]).astype(np.int64)
+    y = (x + h) & 0xFFFFFFFF
+    y = np.minimum(y, (y + q) & 0xFFFFFFFF)
+    y = np.minimum(y, (y - q) & 0xFFFFFFFF)
+    got = y.astype(np.int64) - h
+    assert np.array_equal(got, _centred(x, q))
