@@ -226,6 +226,81 @@ __device__ __forceinline__ void cmux_step(double (&acc0)[E], double (&acc1)[E], 
   for (int e = 0; e < E; ++e) acc1[e] = canon<M>(acc1[e] + accB[e]);
 }
 
+// Level-2 CMUX step on three-buffer exchanges (OMR_XBUF3; xch holds WgNtt::LDS3_DOUBLES).
+// Cross-wave uses of the LDS per step, in order: staging of the mask in X1 (+ a barrier after
+// its reads), the 6 mask-digit NTTs on X1, X0, X1, X0, X1, X0, staging of the body in X1
+// (+ barrier), the 6 body-digit NTTs on X1, X0, ..., the inverse A on X1 and B on X0. Every
+// cross-wave use thus writes a buffer whose last readers have passed a later barrier (the
+// alternation, or the extra barrier after a staging), so no transform needs a trailing barrier:
+// 18 workgroup barriers per step instead of 32. The step starts on X1 and ends on X0.
+template <int T, int E, typename KeyT>
+__device__ __forceinline__ void cmux_step3(double (&acc0)[E], double (&acc1)[E], double *xch, int a,
+                                           const KeyT *__restrict__ ggsw, const double *tw,
+                                           const double *itw, int tid) {
+  using M = Mod<2>;
+  using NTT = WgNtt<M, T, E>;
+  using DG = DigitsFor<2, LOGB2, D2, DROP2>;
+  constexpr int N = M::N;
+  static_assert(D2 % 2 == 0, "digit loop unrolled by two (alternating cross-wave buffers)");
+  double accA[E], accB[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) accA[e] = accB[e] = 0.0;
+  KeyRow<KeyT, E> cur;
+  cur.load(ggsw, N, tid * E);
+  uint32_t pk[E][DG::DW];
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    {  // digits of (X^a - 1) * ACC_p, staged in X1
+      double *st = xch + N;
+#pragma unroll
+      for (int e = 0; e < E; ++e) st[tid + e * T] = p == 0 ? acc0[e] : acc1[e];
+      __syncthreads();
+#pragma unroll
+      for (int e = 0; e < E; ++e)
+        DG::pack(canon_small<M>(rot_read<N>(st, tid + e * T, a) - (p == 0 ? acc0[e] : acc1[e])), pk[e]);
+      __syncthreads();
+    }
+#pragma unroll 1
+    for (int k2 = 0; k2 < D2; k2 += 2) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int k = k2 + h, r = p * D2 + k;
+        double x[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) x[e] = DG::get(pk[e], k);
+        if (h == 0)
+          NTT::template fwd3<1>(x, xch, tw, tid);
+        else
+          NTT::template fwd3<0>(x, xch, tw, tid);
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          accA[e] += mm<M>(x[e], (double)cur.a[e]);
+          accB[e] += mm<M>(x[e], (double)cur.b[e]);
+        }
+        if ((k % 3) == 2) {
+#pragma unroll
+          for (int e = 0; e < E; ++e) {
+            accA[e] = red<M>(accA[e]);
+            accB[e] = red<M>(accB[e]);
+          }
+        }
+        if (r + 1 < 2 * D2) cur.load(ggsw + (size_t)(r + 1) * 2 * N, N, tid * E);
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    accA[e] = red<M>(accA[e]);
+    accB[e] = red<M>(accB[e]);
+  }
+  NTT::template inv3<1>(accA, xch, itw, tid);
+#pragma unroll
+  for (int e = 0; e < E; ++e) acc0[e] = canon<M>(acc0[e] + accA[e]);
+  NTT::template inv3<0>(accB, xch, itw, tid);
+#pragma unroll
+  for (int e = 0; e < E; ++e) acc1[e] = canon<M>(acc1[e] + accB[e]);
+}
+
 // Paired variant: digit k of the mask and digit k of the body are transformed together
 // (two interleaved NTTs sharing every barrier), and the two inverse transforms likewise.
 // xch holds 2N doubles. MAC_EXACT (level 1 only): the transformed digit is reduced to
@@ -566,7 +641,7 @@ __global__ __launch_bounds__(BR2_T, BR2_WAVES) void br2_trace_kernel(const uint3
   using M = Mod<2>;
   constexpr int T = BR2_T, E = BR2_E, N = N2;
   using NTT = WgNtt<M, T, E>;
-  __shared__ double xch[(OMR_PAIR2 ? 2 : 1) * NTT::LDS_DOUBLES];
+  __shared__ double xch[OMR_XBUF3 ? NTT::LDS3_DOUBLES : (OMR_PAIR2 ? 2 : 1) * NTT::LDS_DOUBLES];
   __shared__ double tws[2 * N];
   const int tid = threadIdx.x;
   const size_t wg = blockIdx.x;
@@ -578,7 +653,10 @@ __global__ __launch_bounds__(BR2_T, BR2_WAVES) void br2_trace_kernel(const uint3
   for (int i = 0; i < NI; ++i) {
     const int a = (int)__builtin_amdgcn_readfirstlane(lwe[i]) & (2 * N - 1);
     if (a == 0) continue;
-#if OMR_PAIR2
+#if OMR_XBUF3
+    cmux_step3<T, E, Key2T>(acc0, acc1, xch, a, bsk2 + (size_t)OMR_KEYROW2(i) * (2 * D2 * 2 * N), tw,
+                            itw, tid);
+#elif OMR_PAIR2
     cmux_step_pair<2, T, E, LOGB2, D2, DROP2, Key2T, OMR_KEY_DEPTH2, false>(
         acc0, acc1, xch, a, bsk2 + (size_t)OMR_KEYROW2(i) * (2 * D2 * 2 * N), tw, itw, tid);
 #else
@@ -596,6 +674,7 @@ __global__ __launch_bounds__(BR2_T, BR2_WAVES) void br2_trace_kernel(const uint3
     }
     return;
   }
+  if (OMR_XBUF3) __syncthreads();  // the last inverse's cross-wave reads of X0 are done everywhere
   hom_trace_store(acc0, acc1, xch, tw, itw, tk, tb, o, tid);
 }
 

@@ -19,6 +19,9 @@
 #ifndef OMR_CANON_RED
 #define OMR_CANON_RED 1  // canonical residues by a second rounded reduction (no VCC selects)
 #endif
+#ifndef OMR_XBUF3
+#define OMR_XBUF3 1  // level-2 blind rotation: three-buffer exchanges, one barrier per transform
+#endif
 #ifndef OMR_DB_XCH
 #define OMR_DB_XCH 1  // NTT exchanges through two alternating LDS buffers (fewer barriers)
 #endif
@@ -317,6 +320,68 @@ struct WgNtt {
     static_assert(T == (1 << (L - R)), "pass-0 twiddles uniform only for a full first pass");
     int since_red = 0;
     inv_fromC<NPASS - 1, 1, true>(reinterpret_cast<double(&)[1][E]>(x), lds, itw, tid, since_red, gitw);
+  }
+
+  // ---- three-buffer single transforms (OMR_XBUF3) -------------------------------------------
+  // Cross-wave exchanges use X0 = lds or X1 = lds + N as the caller chooses (XB), wave-local ones
+  // W = lds + 2N, where each wave only ever touches its own slots (the index set a wave owns in
+  // a wave-local pass pair is the same for every such pair). A caller that alternates X0 / X1
+  // between consecutive cross-wave uses of the LDS never writes a buffer that a slower wave may
+  // still read: the other buffer's barrier separates them. No exchange then needs a trailing
+  // barrier, and a transform costs one workgroup barrier (its one cross-wave exchange).
+  static constexpr int LDS3_DOUBLES = 3 * N;
+  template <int PF, int PT, int XB>
+  __device__ static __forceinline__ void exchange3(double (&x)[E], double *lds, int tid) {
+    constexpr bool WL = wave_local(PF, PT);
+    double *buf = lds + (WL ? 2 : XB) * N;
+#pragma unroll
+    for (int e = 0; e < E; ++e) buf[pad(index(PF, tid, e))] = x[e];
+    if constexpr (WL)
+      wave_sync();
+    else
+      __syncthreads();
+#pragma unroll
+    for (int e = 0; e < E; ++e) x[e] = buf[pad(index(PT, tid, e))];
+    // a wave's own LDS operations complete in order; only keep the compiler from hoisting the
+    // next exchange's writes above these reads
+    __builtin_amdgcn_wave_barrier();
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  }
+  static constexpr int cross_wave_exchanges() {
+    int n = 0;
+    for (int p = 1; p < NPASS; ++p) n += wave_local(p - 1, p) ? 0 : 1;
+    return n;
+  }
+  template <int P, int XB>
+  __device__ static __forceinline__ void fwd3_from(double (&x)[E], double *lds, const double *tw,
+                                                   int tid, int &since_red) {
+    if constexpr (P < NPASS) {
+      if constexpr (P > 0) exchange3<P - 1, P, XB>(x, lds, tid);
+      fwd_passC<P, 1>(reinterpret_cast<double(&)[1][E]>(x), tw, tid, since_red);
+      fwd3_from<P + 1, XB>(x, lds, tw, tid, since_red);
+    }
+  }
+  template <int P, int XB>
+  __device__ static __forceinline__ void inv3_from(double (&x)[E], double *lds, const double *itw,
+                                                   int tid, int &since_red) {
+    if constexpr (P >= 0) {
+      if constexpr (P < NPASS - 1) exchange3<P + 1, P, XB>(x, lds, tid);
+      inv_passC<P, 1>(reinterpret_cast<double(&)[1][E]>(x), itw, tid, since_red);
+      inv3_from<P - 1, XB>(x, lds, itw, tid, since_red);
+    }
+  }
+  // XB: the cross-wave buffer (0 / 1) this transform's single cross-wave exchange uses
+  template <int XB>
+  __device__ static __forceinline__ void fwd3(double (&x)[E], double *lds, const double *tw, int tid) {
+    static_assert(cross_wave_exchanges() == 1, "three-buffer scheme written for one cross-wave exchange");
+    int since_red = 0;
+    fwd3_from<0, XB>(x, lds, tw, tid, since_red);
+  }
+  template <int XB>
+  __device__ static __forceinline__ void inv3(double (&x)[E], double *lds, const double *itw, int tid) {
+    static_assert(cross_wave_exchanges() == 1, "three-buffer scheme written for one cross-wave exchange");
+    int since_red = 0;
+    inv3_from<NPASS - 1, XB>(x, lds, itw, tid, since_red);
   }
 
   // Single-transform API.
