@@ -227,12 +227,12 @@ __device__ __forceinline__ void cmux_step(double (&acc0)[E], double (&acc1)[E], 
 }
 
 // Level-2 CMUX step on three-buffer exchanges (OMR_XBUF3; xch holds WgNtt::LDS3_DOUBLES).
-// Cross-wave uses of the LDS per step, in order: staging of the mask in X1 (+ a barrier after
-// its reads), the 6 mask-digit NTTs on X1, X0, X1, X0, X1, X0, staging of the body in X1
-// (+ barrier), the 6 body-digit NTTs on X1, X0, ..., the inverse A on X1 and B on X0. Every
-// cross-wave use thus writes a buffer whose last readers have passed a later barrier (the
-// alternation, or the extra barrier after a staging), so no transform needs a trailing barrier:
-// 18 workgroup barriers per step instead of 32. The step starts on X1 and ends on X0.
+// Cross-wave uses of the LDS per step, in order: staging of the mask in X1, the 6 mask-digit
+// NTTs on X0, X1, X0, X1, X0, X1, staging of the body in X0, the 6 body-digit NTTs on X1, X0,
+// ..., X0, the inverse A on X1 and B on X0; the step starts on X1 and ends on X0. Consecutive
+// cross-wave uses always alternate, so each writes a buffer whose last readers have passed the
+// other buffer's barrier: no transform and no staging needs a trailing barrier, 16 workgroup
+// barriers per step (one per cross-wave use) instead of 32.
 template <int T, int E, typename KeyT>
 __device__ __forceinline__ void cmux_step3(double (&acc0)[E], double (&acc1)[E], double *xch, int a,
                                            const KeyT *__restrict__ ggsw, const double *tw,
@@ -250,15 +250,16 @@ __device__ __forceinline__ void cmux_step3(double (&acc0)[E], double (&acc1)[E],
   uint32_t pk[E][DG::DW];
 #pragma unroll
   for (int p = 0; p < 2; ++p) {
-    {  // digits of (X^a - 1) * ACC_p, staged in X1
-      double *st = xch + N;
+    {  // digits of (X^a - 1) * ACC_p, staged in X1 (mask) / X0 (body)
+      double *st = xch + (p == 0 ? N : 0);
 #pragma unroll
       for (int e = 0; e < E; ++e) st[tid + e * T] = p == 0 ? acc0[e] : acc1[e];
       __syncthreads();
 #pragma unroll
       for (int e = 0; e < E; ++e)
         DG::pack(canon_small<M>(rot_read<N>(st, tid + e * T, a) - (p == 0 ? acc0[e] : acc1[e])), pk[e]);
-      __syncthreads();
+      __builtin_amdgcn_wave_barrier();
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
     }
 #pragma unroll 1
     for (int k2 = 0; k2 < D2; k2 += 2) {
@@ -268,10 +269,10 @@ __device__ __forceinline__ void cmux_step3(double (&acc0)[E], double (&acc1)[E],
         double x[E];
 #pragma unroll
         for (int e = 0; e < E; ++e) x[e] = DG::get(pk[e], k);
-        if (h == 0)
-          NTT::template fwd3<1>(x, xch, tw, tid);
-        else
+        if ((h ^ p) == 0)  // mask digits on X0, X1, ...; body digits on X1, X0, ...
           NTT::template fwd3<0>(x, xch, tw, tid);
+        else
+          NTT::template fwd3<1>(x, xch, tw, tid);
 #pragma unroll
         for (int e = 0; e < E; ++e) {
           accA[e] += mm<M>(x[e], (double)cur.a[e]);
