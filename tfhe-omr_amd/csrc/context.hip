@@ -110,8 +110,13 @@ struct omr_ctx {
   double *tables = nullptr;  // tw1 itw1 tw2 itw2 lut1 lut2
   uint16_t *trace_tabs = nullptr;
   DeviceTables tb{};
-  size_t batch = 16384, batch_cap = 0;
+  size_t batch = OMR_DEFAULT_BATCH, batch_cap = 0;
   uint32_t *ext = nullptr, *lwe1t = nullptr, *lwe_int = nullptr;
+  // OMR_OVERLAP: second stream for level 2 and a second LWE buffer (chunk c's level 2 runs
+  // while chunk c + 1's level 1 does)
+  hipStream_t stream2 = nullptr;
+  uint32_t *lwe_int2 = nullptr;
+  std::vector<hipEvent_t> ov_events;
   // host-API staging
   uint16_t *s_clue_a = nullptr, *s_clue_b = nullptr;
   uint64_t *s_out = nullptr;
@@ -152,6 +157,11 @@ omr_status ensure_batch(omr_ctx *c, size_t B) {
   HIP_TRY(hipMalloc(&c->ext, B * CLUES * (N1 + 1) * sizeof(uint32_t)));
   HIP_TRY(hipMalloc(&c->lwe1t, B * (N1 + 1) * sizeof(uint32_t)));
   HIP_TRY(hipMalloc(&c->lwe_int, B * (NI + 1) * sizeof(uint32_t)));
+  if (OMR_OVERLAP) {
+    hipFree(c->lwe_int2);
+    c->lwe_int2 = nullptr;
+    HIP_TRY(hipMalloc(&c->lwe_int2, B * (NI + 1) * sizeof(uint32_t)));
+  }
   c->batch_cap = B;
   return OMR_OK;
 }
@@ -390,6 +400,12 @@ extern "C" void omr_ctx_destroy(omr_ctx *c) {
                   (void *)c->partial})
     if (p) hipFree(p);
   for (auto e : c->events) hipEventDestroy(e);
+  for (auto e : c->ov_events) hipEventDestroy(e);
+  if (c->stream2) {
+    hipStreamSynchronize(c->stream2);
+    hipStreamDestroy(c->stream2);
+  }
+  if (c->lwe_int2) hipFree(c->lwe_int2);
   if (c->stream) hipStreamDestroy(c->stream);
   delete c;
 }
@@ -402,7 +418,7 @@ extern "C" const char *omr_detect_kernels(void) {
 extern "C" omr_status omr_ctx_set_batch(omr_ctx *c, size_t batch) {
   if (!c) return set_error(OMR_ERR_INVALID_ARGUMENT, "omr_ctx_set_batch: NULL ctx");
   std::lock_guard<std::mutex> lk(c->mu);
-  c->batch = batch ? batch : 16384;
+  c->batch = batch ? batch : OMR_DEFAULT_BATCH;
   hipSetDevice(c->device);
   return ensure_batch(c, c->batch);
 }
@@ -414,6 +430,49 @@ extern "C" omr_status omr_ctx_enable_timing(omr_ctx *c, int enable) {
 }
 
 namespace {
+
+// OMR_OVERLAP (experiment): level 1 + key switch of chunk c + 1 on st while level 2 of chunk c
+// runs on stream2; LWE buffers alternate, each reused only after the level 2 that read it.
+// Stage events: [0] br1 start, [1] br1 end, [2] ks end (st), [4] br2 start, [3] br2 end (stream2).
+omr_status detect_device_overlap(omr_ctx *c, const uint16_t *ca, const uint16_t *cb, size_t D,
+                                 uint64_t *out, hipStream_t st, size_t nchunks) {
+  if (!c->stream2) HIP_TRY(hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));
+  while (c->ov_events.size() < 2 * nchunks + 1) {
+    hipEvent_t e;
+    HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    c->ov_events.push_back(e);
+  }
+  hipEvent_t *ks_done = &c->ov_events[0], *br2_done = &c->ov_events[nchunks],
+             start = c->ov_events[2 * nchunks];
+  HIP_TRY(hipEventRecord(start, st));
+  HIP_TRY(hipStreamWaitEvent(c->stream2, start, 0));  // level 2 starts after the caller's prior work
+  for (size_t ch = 0; ch < nchunks; ++ch) {
+    const size_t off = ch * c->batch;
+    const int B = (int)std::min(c->batch, D - off);
+    uint32_t *lwe = (ch & 1) ? c->lwe_int2 : c->lwe_int;
+    hipEvent_t *ev = c->timing ? &c->events[ch * 5] : nullptr;
+    omr_status s;
+    if (ev) HIP_TRY(hipEventRecord(ev[0], st));
+    if ((s = launch_br1(c, (size_t)B * CLUES, ca + off * N0, cb + off * CLUES, nullptr, nullptr,
+                        c->ext, nullptr, 0, st)) != OMR_OK)
+      return s;
+    if (ev) HIP_TRY(hipEventRecord(ev[1], st));
+    const size_t n7 = (size_t)B * (N1 + 1);
+    sum7_kernel<<<(unsigned)((n7 + 255) / 256), 256, 0, st>>>(c->ext, c->lwe1t, B);
+    if (ch >= 2) HIP_TRY(hipStreamWaitEvent(st, br2_done[ch - 2], 0));  // its LWE buffer is free
+    ks_kernel<KS_CT><<<dim3((B + 63) / 64, (NI + 1 + KS_CT - 1) / KS_CT), 64, 0, st>>>(c->lwe1t, c->ksk, lwe, B);
+    HIP_TRY(hipGetLastError());
+    if (ev) HIP_TRY(hipEventRecord(ev[2], st));
+    HIP_TRY(hipEventRecord(ks_done[ch], st));
+    HIP_TRY(hipStreamWaitEvent(c->stream2, ks_done[ch], 0));
+    if (ev) HIP_TRY(hipEventRecord(ev[4], c->stream2));
+    if ((s = launch_br2(c, (size_t)B, lwe, out + off * 2 * N2, 0, c->stream2)) != OMR_OK) return s;
+    if (ev) HIP_TRY(hipEventRecord(ev[3], c->stream2));
+    HIP_TRY(hipEventRecord(br2_done[ch], c->stream2));
+  }
+  HIP_TRY(hipStreamWaitEvent(st, br2_done[nchunks - 1], 0));  // the caller's stream sees the output
+  return OMR_OK;
+}
 
 omr_status detect_device(omr_ctx *c, const uint16_t *ca, const uint16_t *cb, size_t D,
                          uint64_t *out, hipStream_t st) {
@@ -428,6 +487,7 @@ omr_status detect_device(omr_ctx *c, const uint16_t *ca, const uint16_t *cb, siz
     }
     c->timed_messages = D;
   }
+  if (OMR_OVERLAP) return detect_device_overlap(c, ca, cb, D, out, st, nchunks);
   for (size_t ch = 0; ch < nchunks; ++ch) {
     const size_t off = ch * c->batch;
     const int B = (int)std::min(c->batch, D - off);
@@ -507,7 +567,7 @@ extern "C" omr_status omr_last_timing(omr_ctx *c, omr_detect_timing *t) {
     float a = 0, b = 0, d = 0;
     HIP_TRY(hipEventElapsedTime(&a, ev[0], ev[1]));
     HIP_TRY(hipEventElapsedTime(&b, ev[1], ev[2]));
-    HIP_TRY(hipEventElapsedTime(&d, ev[2], ev[3]));
+    HIP_TRY(hipEventElapsedTime(&d, OMR_OVERLAP ? ev[4] : ev[2], ev[3]));
     t->first_level_ms += a;
     t->key_switch_ms += b;
     t->second_level_ms += d;

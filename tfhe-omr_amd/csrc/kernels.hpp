@@ -52,6 +52,12 @@ namespace omr {
 #ifndef OMR_BR2_SLICED
 #define OMR_BR2_SLICED 0  // level 2: sliced exact-FFT kernel (br2_sliced.hpp); implies FFT-form keys
 #endif
+#ifndef OMR_DEFAULT_BATCH
+#define OMR_DEFAULT_BATCH 16384  // messages per detect chunk (scratch 36 KiB/msg)
+#endif
+#ifndef OMR_OVERLAP
+#define OMR_OVERLAP 0     // detect: level 2 of chunk c on a second stream beside level 1 of chunk c + 1
+#endif
 #ifndef OMR_NTT_GTW
 #define OMR_NTT_GTW 0     // level 2: pass-0 NTT twiddles (workgroup-uniform) by scalar loads (+1.5 %: off)
 #endif
