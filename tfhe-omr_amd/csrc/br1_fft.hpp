@@ -36,6 +36,9 @@ namespace omr {
 #define BR1F_BARRIERS 2  // workgroup barriers per staged key row (1: next row issued after the MAC barrier;
                          // exposes the row latency: 212 vs 199 ms at D = 4,096)
 #endif
+#ifndef BR1F_KBUF
+#define BR1F_KBUF 2  // staged key-row buffers: 2 (two barriers per row) or 3 (one; needs BR1F_WPG 8 to fit LDS)
+#endif
 #ifndef BR1F_DIGIT_SBFE
 #define BR1F_DIGIT_SBFE 2  // digit words in two's-complement fields; 2: two uniform shifts per digit, 1: v_bfe_i32 (inline asm, slower)
 #endif
@@ -275,9 +278,13 @@ __device__ __forceinline__ void br1f_step_lds(int (&ac)[2][16], double2 *xch, co
     for (int k = 0; k < D1; ++k) {
       const int q = q0 + p * D1 + k;
       const bool more = q + 1 < qtotal;
-#if BR1F_BARRIERS == 2
+#if BR1F_BARRIERS == 2 && BR1F_KBUF == 2
+#if !defined(OMR_EXPT_NO_KSTAGE) && !defined(OMR_EXPT_KSTAGE_NOBAR)  // timing experiments only
       wg_barrier_lds();  // every wave has finished reading buffer (q + 1) & 1 (row q - 1)
+#endif
+#ifndef OMR_EXPT_NO_KSTAGE
       if (more) krow_issue(bskf + (size_t)(q + 1) * KROW_SLOTS, kbuf + ((q + 1) & 1) * KROW_SLOTS, lane, wave);
+#endif
 #endif
       double xr[8], xi[8];
 #pragma unroll
@@ -286,18 +293,33 @@ __device__ __forceinline__ void br1f_step_lds(int (&ac)[2][16], double2 *xch, co
         xi[e] = Lvl1Int::digit(pk[p][8 + e], k);
       }
       F::fwd<1, BR1F_GTW != 0>(reinterpret_cast<X>(xr), reinterpret_cast<X>(xi), xch, tws, lane, gtw);
-#if BR1F_BARRIERS == 2
+#if BR1F_KBUF == 3
+      // three staged rows, one barrier per row: row q landed (row q + 1 may stay in flight) in
+      // every wave's share, and every wave is past its multiply-accumulate of row q - 1, so
+      // buffer (q + 2) % 3 = (q - 1) % 3 is free for row q + 2
+      if (more)
+        vm_wait_row_in_flight();
+      else
+        vm_wait_all();
+      wg_barrier_lds();
+      if (q + 2 < qtotal)
+        krow_issue(bskf + (size_t)(q + 2) * KROW_SLOTS, kbuf + ((q + 2) % 3) * KROW_SLOTS, lane, wave);
+#elif BR1F_BARRIERS == 2
+#ifndef OMR_EXPT_NO_KSTAGE
       if (more)
         vm_wait_row_in_flight();  // row q landed (row q + 1 may stay in flight)
       else
         vm_wait_all();
+#endif
+#if !defined(OMR_EXPT_NO_KSTAGE) && !defined(OMR_EXPT_KSTAGE_NOBAR)
       wg_barrier_lds();  // ... in every wave's share
+#endif
 #else
       vm_wait_all();     // this wave's share of row q landed (the only copy in flight)
       wg_barrier_lds();  // row q complete, and every wave is done with row q - 1 (its buffer)
       if (more) krow_issue(bskf + (size_t)(q + 1) * KROW_SLOTS, kbuf + ((q + 1) & 1) * KROW_SLOTS, lane, wave);
 #endif
-      const double2 *kb = kbuf + (q & 1) * KROW_SLOTS;
+      const double2 *kb = kbuf + (BR1F_KBUF == 3 ? q % 3 : q & 1) * KROW_SLOTS;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const double2 ka = kb[e * 64 + lane], kB = kb[F::N + e * 64 + lane];
@@ -336,7 +358,7 @@ __global__ __launch_bounds__(64 * BR1F_WPG, BR1F_WAVES) void br1f_kernel(
   __shared__ uint16_t la_all[W][RW][N0];
 #if BR1F_KEY_LDS
   static_assert(RW == 1 && 16 % W == 0, "LDS key staging: one rotation per wave, W divides 16");
-  __shared__ double2 kbuf[2 * KROW_SLOTS];
+  __shared__ double2 kbuf[BR1F_KBUF * KROW_SLOTS];
 #endif
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   double2 *xch = xch_all[wave];
@@ -376,6 +398,7 @@ __global__ __launch_bounds__(64 * BR1F_WPG, BR1F_WAVES) void br1f_kernel(
   // every step runs (a = 0 gives zero digits and leaves ACC unchanged) so the waves share the
   // staged key rows; row 0 is issued before the loop
   krow_issue(bskf, kbuf, lane, wave);
+  if (BR1F_KBUF == 3) krow_issue(bskf + KROW_SLOTS, kbuf + KROW_SLOTS, lane, wave);
 #pragma unroll 1
   for (int i = 0; i < N0; ++i) {
     int a[RW];
