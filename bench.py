@@ -161,6 +161,10 @@ def end_to_end(det, pack_a, d_out, D, first, total, pert, dist, dev, stream, ran
 
 def main():
     args = parse()
+    # The JSON line is the only thing on stdout: keep a handle on the real stdout and send fd 1
+    # (library chatter, e.g. RCCL's version banner at communicator init) to stderr.
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     import torch
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -329,7 +333,7 @@ def main():
                               for b, shape in zip(kbufs, (A.BSK1_SHAPE, A.KSK_SHAPE, A.BSK2_SHAPE, A.TK_SHAPE))])
         line["cpu_baseline"] = cpu_baseline(dk, d_ca[:n].cpu().numpy().view(np.uint16),
                                             d_cb[:n].cpu().numpy().view(np.uint16), n)
-    print(json.dumps(line), flush=True)
+    print(json.dumps(line), file=json_out, flush=True)
     if dist:
         dist.destroy_process_group()
 
