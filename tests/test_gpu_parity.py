@@ -254,8 +254,14 @@ def test_edge_inputs_bit_exact(real):
     det.set_batch(5)
     try:
         got = det.detect_batch(ca, cb)
+        # detect_with_time_info over host buffers staged in pieces of the batch size: the stage
+        # times and the message count cover the whole call, not only its last piece
+        got_t, info = det.detect_with_time_info(ca, cb)
     finally:
         det.set_batch(0)
     assert np.array_equal(got, orc.detect_batch(ca, cb))
+    assert np.array_equal(got_t, got)
+    assert info["messages"] == 12 and info["first_level_ms"] > 0 and info["second_level_ms"] > 0
+    assert abs(info["total_ms"] - info["first_level_ms"] - info["key_switch_ms"] - info["second_level_ms"]) < 1e-3 * info["total_ms"] + 1e-3
     empty = det.detect_batch(np.zeros((0, A.N0), np.uint16), np.zeros((0, A.CLUE_COUNT), np.uint16))
     assert empty.shape == (0, 2, A.N2)

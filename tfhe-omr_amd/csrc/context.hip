@@ -123,6 +123,10 @@ struct omr_ctx {
   size_t staged = 0;
   // encode workspace
   uint64_t *partial = nullptr;
+  // omr_detect_batch stages the host input in pieces of `batch` messages: their stage times are
+  // summed here so omr_last_timing covers the whole call (device-buffer calls read the events)
+  omr_detect_timing host_timing{};
+  bool host_timing_valid = false;
   size_t partial_cap = 0;
   // timing
   bool timing = false;
@@ -532,7 +536,12 @@ extern "C" omr_status omr_detect_batch_device(omr_ctx *c, const uint16_t *ca, co
   if (D == 0) return OMR_OK;
   std::lock_guard<std::mutex> lk(c->mu);
   HIP_TRY(hipSetDevice(c->device));
+  c->host_timing_valid = false;
   return detect_device(c, ca, cb, D, out, stream ? (hipStream_t)stream : c->stream);
+}
+
+namespace {
+omr_status collect_timing(omr_ctx *c, omr_detect_timing *t);
 }
 
 extern "C" omr_status omr_detect_batch(omr_ctx *c, const uint16_t *ca, const uint16_t *cb, size_t D,
@@ -545,6 +554,8 @@ extern "C" omr_status omr_detect_batch(omr_ctx *c, const uint16_t *ca, const uin
   omr_status s;
   const size_t B = std::min(D, c->batch);
   if ((s = stage_buffers(c, B)) != OMR_OK) return s;
+  omr_detect_timing acc{};
+  c->host_timing_valid = false;
   for (size_t off = 0; off < D; off += B) {
     const size_t n = std::min(B, D - off);
     HIP_TRY(hipMemcpyAsync(c->s_clue_a, ca + off * N0, n * N0 * sizeof(uint16_t), hipMemcpyHostToDevice, c->stream));
@@ -552,12 +563,26 @@ extern "C" omr_status omr_detect_batch(omr_ctx *c, const uint16_t *ca, const uin
     if ((s = detect_device(c, c->s_clue_a, c->s_clue_b, n, c->s_out, c->stream)) != OMR_OK) return s;
     HIP_TRY(hipMemcpyAsync(out + off * 2 * N2, c->s_out, n * 2 * N2 * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
+    if (c->timing) {
+      omr_detect_timing t;
+      if ((s = collect_timing(c, &t)) != OMR_OK) return s;
+      acc.first_level_ms += t.first_level_ms;
+      acc.key_switch_ms += t.key_switch_ms;
+      acc.second_level_ms += t.second_level_ms;
+      acc.total_ms += t.total_ms;
+      acc.messages += t.messages;
+    }
+  }
+  if (c->timing) {
+    c->host_timing = acc;
+    c->host_timing_valid = true;
   }
   return OMR_OK;
 }
 
-extern "C" omr_status omr_last_timing(omr_ctx *c, omr_detect_timing *t) {
-  if (!c || !t) return set_error(OMR_ERR_INVALID_ARGUMENT, "omr_last_timing: NULL argument");
+namespace {
+// Stage times of the last detect_device call from its per-chunk events.
+omr_status collect_timing(omr_ctx *c, omr_detect_timing *t) {
   memset(t, 0, sizeof(*t));
   if (!c->timing || c->timed_messages == 0) return OMR_OK;
   const size_t nchunks = (c->timed_messages + c->batch - 1) / c->batch;
@@ -575,6 +600,16 @@ extern "C" omr_status omr_last_timing(omr_ctx *c, omr_detect_timing *t) {
   t->total_ms = t->first_level_ms + t->key_switch_ms + t->second_level_ms;
   t->messages = c->timed_messages;
   return OMR_OK;
+}
+}  // namespace
+
+extern "C" omr_status omr_last_timing(omr_ctx *c, omr_detect_timing *t) {
+  if (!c || !t) return set_error(OMR_ERR_INVALID_ARGUMENT, "omr_last_timing: NULL argument");
+  if (c->host_timing_valid) {
+    *t = c->host_timing;
+    return OMR_OK;
+  }
+  return collect_timing(c, t);
 }
 
 // ------------------------------------------------------------------------------------------
