@@ -257,21 +257,26 @@ __device__ __forceinline__ void wg_barrier_lds() {  // LDS reads/writes done, th
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
 }
 
-// One CMUX step with LDS-staged key rows. q0 = first global row of this step; rows q0..q0+7 are
-// consumed, row q0+8 (next step's first) is prefetched at the end. kbuf: 2 staged rows.
-__device__ __forceinline__ void br1f_step_lds(int (&ac)[2][16], double2 *xch, const double2 *tws,
-                                              int a, const double2 *__restrict__ bskf, int q0,
-                                              int qtotal, double2 *kbuf, int lane, int wave,
+// One CMUX step with LDS-staged key rows for the RW rotations of this wave (their transforms
+// interleaved, each staged key value read once for all of them). q0 = first global row of this
+// step; rows q0..q0+7 are consumed, the next step's first row(s) are prefetched on the way.
+// xch: RW exchange buffers of Fft512::BUF.
+template <int RW>
+__device__ __forceinline__ void br1f_step_lds(int (&ac)[RW][2][16], double2 *xch, const double2 *tws,
+                                              const int (&a)[RW], const double2 *__restrict__ bskf,
+                                              int q0, int qtotal, double2 *kbuf, int lane, int wave,
                                               const double2 *__restrict__ gtw) {
   using F = Fft512;
-  using X = double(&)[1][8];
-  uint32_t pk[2][16];
-  br1f_digits(ac, reinterpret_cast<int *>(xch), a, lane, pk);
-  double outr[2][8], outi[2][8];
+  uint32_t pk[RW][2][16];
+#pragma unroll
+  for (int r = 0; r < RW; ++r) br1f_digits(ac[r], reinterpret_cast<int *>(xch + r * F::BUF), a[r], lane, pk[r]);
+  double outr[2][RW][8], outi[2][RW][8];
 #pragma unroll
   for (int o = 0; o < 2; ++o)
 #pragma unroll
-    for (int e = 0; e < 8; ++e) outr[o][e] = outi[o][e] = 0.0;
+    for (int r = 0; r < RW; ++r)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) outr[o][r][e] = outi[o][r][e] = 0.0;
 #pragma unroll
   for (int p = 0; p < 2; ++p) {
 #pragma unroll 1
@@ -286,13 +291,15 @@ __device__ __forceinline__ void br1f_step_lds(int (&ac)[2][16], double2 *xch, co
       if (more) krow_issue(bskf + (size_t)(q + 1) * KROW_SLOTS, kbuf + ((q + 1) & 1) * KROW_SLOTS, lane, wave);
 #endif
 #endif
-      double xr[8], xi[8];
+      double xr[RW][8], xi[RW][8];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        xr[e] = Lvl1Int::digit(pk[p][e], k);
-        xi[e] = Lvl1Int::digit(pk[p][8 + e], k);
-      }
-      F::fwd<1, BR1F_GTW != 0>(reinterpret_cast<X>(xr), reinterpret_cast<X>(xi), xch, tws, lane, gtw);
+      for (int r = 0; r < RW; ++r)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          xr[r][e] = Lvl1Int::digit(pk[r][p][e], k);
+          xi[r][e] = Lvl1Int::digit(pk[r][p][8 + e], k);
+        }
+      F::fwd<RW, BR1F_GTW != 0>(xr, xi, xch, tws, lane, gtw);
 #if BR1F_KBUF == 3
       // three staged rows, one barrier per row: row q landed (row q + 1 may stay in flight) in
       // every wave's share, and every wave is past its multiply-accumulate of row q - 1, so
@@ -323,21 +330,26 @@ __device__ __forceinline__ void br1f_step_lds(int (&ac)[2][16], double2 *xch, co
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const double2 ka = kb[e * 64 + lane], kB = kb[F::N + e * 64 + lane];
-        outr[0][e] = __fma_rn(xr[e], ka.x, __fma_rn(-xi[e], ka.y, outr[0][e]));
-        outi[0][e] = __fma_rn(xr[e], ka.y, __fma_rn(xi[e], ka.x, outi[0][e]));
-        outr[1][e] = __fma_rn(xr[e], kB.x, __fma_rn(-xi[e], kB.y, outr[1][e]));
-        outi[1][e] = __fma_rn(xr[e], kB.y, __fma_rn(xi[e], kB.x, outi[1][e]));
+#pragma unroll
+        for (int r = 0; r < RW; ++r) {
+          outr[0][r][e] = __fma_rn(xr[r][e], ka.x, __fma_rn(-xi[r][e], ka.y, outr[0][r][e]));
+          outi[0][r][e] = __fma_rn(xr[r][e], ka.y, __fma_rn(xi[r][e], ka.x, outi[0][r][e]));
+          outr[1][r][e] = __fma_rn(xr[r][e], kB.x, __fma_rn(-xi[r][e], kB.y, outr[1][r][e]));
+          outi[1][r][e] = __fma_rn(xr[r][e], kB.y, __fma_rn(xi[r][e], kB.x, outi[1][r][e]));
+        }
       }
     }
   }
 #pragma unroll
   for (int o = 0; o < 2; ++o) {
-    F::inv<1, BR1F_GTW != 0>(reinterpret_cast<X>(outr[o]), reinterpret_cast<X>(outi[o]), xch, tws, lane, gtw);
+    F::inv<RW, BR1F_GTW != 0>(outr[o], outi[o], xch, tws, lane, gtw);
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const double v = rint(i < 8 ? outr[o][i] : outi[o][i - 8]);  // exact (< 2^43)
-      ac[o][i] = Lvl1Int::canon(ac[o][i] + (int)red<Mod<1>>(v));
-    }
+    for (int r = 0; r < RW; ++r)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const double v = rint(i < 8 ? outr[o][r][i] : outi[o][r][i - 8]);  // exact (< 2^43)
+        ac[r][o][i] = Lvl1Int::canon(ac[r][o][i] + (int)red<Mod<1>>(v));
+      }
   }
 }
 
@@ -357,7 +369,7 @@ __global__ __launch_bounds__(64 * BR1F_WPG, BR1F_WAVES) void br1f_kernel(
   __shared__ double2 tws[NF];
   __shared__ uint16_t la_all[W][RW][N0];
 #if BR1F_KEY_LDS
-  static_assert(RW == 1 && 16 % W == 0, "LDS key staging: one rotation per wave, W divides 16");
+  static_assert(16 % W == 0, "LDS key staging: W divides the row's 16 one-KiB pieces");
   __shared__ double2 kbuf[BR1F_KBUF * KROW_SLOTS];
 #endif
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -402,8 +414,9 @@ __global__ __launch_bounds__(64 * BR1F_WPG, BR1F_WAVES) void br1f_kernel(
 #pragma unroll 1
   for (int i = 0; i < N0; ++i) {
     int a[RW];
-    a[0] = __builtin_amdgcn_readfirstlane(la[0][i]);
-    br1f_step_lds(ac[0], xch, tws, a[0], bskf, i * 2 * D1, N0 * 2 * D1, kbuf, lane, wave, tb.fft1);
+#pragma unroll
+    for (int r = 0; r < RW; ++r) a[r] = __builtin_amdgcn_readfirstlane(la[r][i]);
+    br1f_step_lds<RW>(ac, xch, tws, a, bskf, i * 2 * D1, N0 * 2 * D1, kbuf, lane, wave, tb.fft1);
   }
   __syncthreads();
 #else
