@@ -667,6 +667,9 @@ __global__ __launch_bounds__(BR2_T, BR2_WAVES) void br2_trace_kernel(const uint3
 #endif
   }
   uint64_t *o = out + wg * 2 * N;
+#ifdef OMR_EXPT_NO_TRACE  // timing experiment only (wrong results): blind rotation without the trace
+  mode = 1;
+#endif
   if (mode == 1) {
 #pragma unroll
     for (int e = 0; e < E; ++e) {
