@@ -107,6 +107,7 @@ struct omr_ctx {
   double2 *bsk2f = nullptr; // level-2 FFT-domain key limbs (OMR_FFT2)
   double *bsk2 = nullptr, *tk = nullptr;
   uint32_t *ksk = nullptr;
+  uint32_t *kskb = nullptr;  // OMR_KS_MFMA: int8 limbs of the KSK, [1024][4][672][32]
   double *tables = nullptr;  // tw1 itw1 tw2 itw2 lut1 lut2
   uint16_t *trace_tabs = nullptr;
   DeviceTables tb{};
@@ -211,6 +212,16 @@ omr_status convert_keys_fft1(const uint32_t *host, size_t npoly, double2 *dev, c
     HIP_TRY(hipStreamSynchronize(st));
   }
   hipFree(tmp);
+  return OMR_OK;
+}
+
+// LWE key switch + modulus switch of B messages (lwe1t [1025][B] -> out [B][671]).
+omr_status launch_ks(omr_ctx *c, int B, uint32_t *out, hipStream_t st) {
+  if (OMR_KS_MFMA)
+    ks_mfma_kernel<<<dim3((B + 63) / 64, KSM_COLS / 32), 64, 0, st>>>(c->lwe1t, c->kskb, out, B);
+  else
+    ks_kernel<KS_CT><<<dim3((B + 63) / 64, (NI + 1 + KS_CT - 1) / KS_CT), 64, 0, st>>>(c->lwe1t, c->ksk, out, B);
+  HIP_TRY(hipGetLastError());
   return OMR_OK;
 }
 
@@ -389,6 +400,13 @@ extern "C" omr_status omr_ctx_create(const omr_detection_key_view *key, int devi
       hipMemsetAsync(c->ksk + KSK_ELEMS, 0, 64 * sizeof(uint32_t), c->stream) != hipSuccess ||
       hipStreamSynchronize(c->stream) != hipSuccess)
     return fail(set_error(OMR_ERR_DEVICE, "omr_ctx_create: key upload"));
+  if (OMR_KS_MFMA) {  // int8 limbs of the KSK for the matrix-core key switch (88 MB)
+    if (hipMalloc(&c->kskb, KSKB_WORDS * sizeof(uint32_t)) != hipSuccess)
+      return fail(set_error(OMR_ERR_OUT_OF_MEMORY, "omr_ctx_create: KSK limbs"));
+    ksk_to_i8_kernel<<<(unsigned)((KSKB_WORDS + 255) / 256), 256, 0, c->stream>>>(c->ksk, c->kskb);
+    if (hipGetLastError() != hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess)
+      return fail(set_error(OMR_ERR_DEVICE, "omr_ctx_create: KSK limbs"));
+  }
   if ((st = ensure_batch(c, c->batch)) != OMR_OK) return fail(st);
   *out = c;
   return OMR_OK;
@@ -398,7 +416,7 @@ extern "C" void omr_ctx_destroy(omr_ctx *c) {
   if (!c) return;
   hipSetDevice(c->device);
   if (c->stream) hipStreamSynchronize(c->stream);
-  for (void *p : {(void *)c->bsk1, (void *)c->bsk1f, (void *)c->fft1, (void *)c->fft2, (void *)c->fft2w, (void *)c->bsk2f, (void *)c->bsk2, (void *)c->tk, (void *)c->ksk,
+  for (void *p : {(void *)c->bsk1, (void *)c->bsk1f, (void *)c->fft1, (void *)c->fft2, (void *)c->fft2w, (void *)c->bsk2f, (void *)c->bsk2, (void *)c->tk, (void *)c->ksk, (void *)c->kskb,
                   (void *)c->tables, (void *)c->trace_tabs, (void *)c->ext, (void *)c->lwe1t,
                   (void *)c->lwe_int, (void *)c->s_clue_a, (void *)c->s_clue_b, (void *)c->s_out,
                   (void *)c->partial})
@@ -464,8 +482,7 @@ omr_status detect_device_overlap(omr_ctx *c, const uint16_t *ca, const uint16_t 
     const size_t n7 = (size_t)B * (N1 + 1);
     sum7_kernel<<<(unsigned)((n7 + 255) / 256), 256, 0, st>>>(c->ext, c->lwe1t, B);
     if (ch >= 2) HIP_TRY(hipStreamWaitEvent(st, br2_done[ch - 2], 0));  // its LWE buffer is free
-    ks_kernel<KS_CT><<<dim3((B + 63) / 64, (NI + 1 + KS_CT - 1) / KS_CT), 64, 0, st>>>(c->lwe1t, c->ksk, lwe, B);
-    HIP_TRY(hipGetLastError());
+    if ((s = launch_ks(c, B, lwe, st)) != OMR_OK) return s;
     if (ev) HIP_TRY(hipEventRecord(ev[2], st));
     HIP_TRY(hipEventRecord(ks_done[ch], st));
     HIP_TRY(hipStreamWaitEvent(c->stream2, ks_done[ch], 0));
@@ -503,8 +520,7 @@ omr_status detect_device(omr_ctx *c, const uint16_t *ca, const uint16_t *cb, siz
     if (ev) HIP_TRY(hipEventRecord(ev[1], st));
     const size_t n7 = (size_t)B * (N1 + 1);
     sum7_kernel<<<(unsigned)((n7 + 255) / 256), 256, 0, st>>>(c->ext, c->lwe1t, B);
-    ks_kernel<KS_CT><<<dim3((B + 63) / 64, (NI + 1 + KS_CT - 1) / KS_CT), 64, 0, st>>>(c->lwe1t, c->ksk, c->lwe_int, B);
-    HIP_TRY(hipGetLastError());
+    if ((s = launch_ks(c, B, c->lwe_int, st)) != OMR_OK) return s;
     if (ev) HIP_TRY(hipEventRecord(ev[2], st));
     if ((s = launch_br2(c, (size_t)B, c->lwe_int, out + off * 2 * N2, 0, st)) != OMR_OK) return s;
     if (ev) HIP_TRY(hipEventRecord(ev[3], st));
@@ -744,7 +760,10 @@ extern "C" omr_status omr_first_level(omr_ctx *c, const uint16_t *ca, const uint
     return s;
   const size_t n7 = (size_t)B * (N1 + 1);
   sum7_kernel<<<(unsigned)((n7 + 255) / 256), 256, 0, st>>>(c->ext, c->lwe1t, B);
-  ks_kernel<KS_CT><<<dim3((B + 63) / 64, (NI + 1 + KS_CT - 1) / KS_CT), 64, 0, st>>>(c->lwe1t, c->ksk, c->lwe_int, B);
+  {
+    omr_status ks;
+    if ((ks = launch_ks(c, B, c->lwe_int, st)) != OMR_OK) return ks;
+  }
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(lwe_int, c->lwe_int, D * (NI + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));

@@ -538,6 +538,12 @@ __global__ __launch_bounds__(64) void ks_kernel(const uint32_t *__restrict__ lwe
 }
 constexpr int KS_CT = 16;
 
+}  // namespace omr
+
+#include "ks_mfma.hpp"
+
+namespace omr {
+
 // hom_trace (detector.rs:626-639) of the level-2 accumulator (coefficient layout tid + e*T,
 // canonical) and store of NTT(c) as NttRlweCiphertext u64 [2][N2] at o. tw/itw: NTT twiddles in
 // LDS; xch: N2 doubles of LDS.

@@ -52,6 +52,9 @@ namespace omr {
 #ifndef OMR_BR2_SLICED
 #define OMR_BR2_SLICED 0  // level 2: sliced exact-FFT kernel (br2_sliced.hpp); implies FFT-form keys
 #endif
+#ifndef OMR_KS_MFMA
+#define OMR_KS_MFMA 1     // LWE key switch as an int8 GEMM on the matrix cores (ks_mfma.hpp)
+#endif
 #ifndef OMR_DEFAULT_BATCH
 #define OMR_DEFAULT_BATCH 16384  // messages per detect chunk (scratch 36 KiB/msg)
 #endif
