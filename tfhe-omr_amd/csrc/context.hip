@@ -141,6 +141,11 @@ struct omr_ctx {
 #else
 #define OMR_BR1_NAME "br1_kernel"
 #endif
+#if OMR_KS_MFMA
+#define OMR_KS_NAME "ks_mfma_kernel"
+#else
+#define OMR_KS_NAME "ks_kernel"
+#endif
 #if OMR_BR2_SLICED
 #define OMR_BR2_NAME "br2s_trace_kernel"
 #elif OMR_FFT2
@@ -434,7 +439,7 @@ extern "C" void omr_ctx_destroy(omr_ctx *c) {
 
 // Names of the detect-path kernels this build launches (bench.py / profile summaries).
 extern "C" const char *omr_detect_kernels(void) {
-  return "br1=" OMR_BR1_NAME " ks=ks_kernel br2=" OMR_BR2_NAME;
+  return "br1=" OMR_BR1_NAME " ks=" OMR_KS_NAME " br2=" OMR_BR2_NAME;
 }
 
 extern "C" omr_status omr_ctx_set_batch(omr_ctx *c, size_t batch) {
