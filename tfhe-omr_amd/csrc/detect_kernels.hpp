@@ -37,13 +37,14 @@ struct Digits8 {
       pk[k / 4] |= ((uint32_t)(int)d & 0xffu) << (8 * (k % 4));
     }
   }
-  __device__ static __forceinline__ double get(const uint32_t (&pk)[DW], int k) {
+  __device__ static __forceinline__ int get_int(const uint32_t (&pk)[DW], int k) {
     uint32_t w = pk[0];
 #pragma unroll
     for (int i = 1; i < DW; ++i) w = (k >> 2) == i ? pk[i] : w;
     const int s = 24 - 8 * (k & 3);
-    return (double)((int32_t)(w << s) >> 24);
+    return (int32_t)(w << s) >> 24;
   }
+  __device__ static __forceinline__ double get(const uint32_t (&pk)[DW], int k) { return (double)get_int(pk, k); }
 };
 
 // Level-2 gadget digits (logB 7, d 6, drop 8) in closed form: y = floor((v + 2^7) / 2^8) has
@@ -61,12 +62,13 @@ struct Digits2 {
     pk[0] = (uint32_t)(int)lo;
     pk[1] = (uint32_t)(int)hi;
   }
-  __device__ static __forceinline__ double get(const uint32_t (&pk)[DW], int k) {
-    if (k == D2 - 1) return (double)((int)pk[1] >> 14);
+  __device__ static __forceinline__ int get_int(const uint32_t (&pk)[DW], int k) {
+    if (k == D2 - 1) return (int)pk[1] >> 14;
     const uint32_t w = k < 3 ? pk[0] : pk[1];
     const int sh = 7 * (k < 3 ? k : k - 3);
-    return (double)((int)((w >> sh) & 127u) - 64);
+    return (int)((w >> sh) & 127u) - 64;
   }
+  __device__ static __forceinline__ double get(const uint32_t (&pk)[DW], int k) { return (double)get_int(pk, k); }
 };
 template <int LEVEL, int LOGB, int D, int DROP>
 using DigitsFor = std::conditional_t<LEVEL == 2 && OMR_DIGITS2_CLOSED, Digits2, Digits8<LOGB, D, DROP>>;
@@ -236,7 +238,7 @@ __device__ __forceinline__ void cmux_step(double (&acc0)[E], double (&acc1)[E], 
 template <int T, int E, typename KeyT>
 __device__ __forceinline__ void cmux_step3(double (&acc0)[E], double (&acc1)[E], double *xch, int a,
                                            const KeyT *__restrict__ ggsw, const double *tw,
-                                           const double *itw, int tid) {
+                                           const double *itw, int tid, const double *t0 = nullptr) {
   using M = Mod<2>;
   using NTT = WgNtt<M, T, E>;
   using DG = DigitsFor<2, LOGB2, D2, DROP2>;
@@ -267,12 +269,22 @@ __device__ __forceinline__ void cmux_step3(double (&acc0)[E], double (&acc1)[E],
       for (int h = 0; h < 2; ++h) {
         const int k = k2 + h, r = p * D2 + k;
         double x[E];
+        if (OMR_NTT_SMALL0) {
+          int d[E];
 #pragma unroll
-        for (int e = 0; e < E; ++e) x[e] = DG::get(pk[e], k);
-        if ((h ^ p) == 0)  // mask digits on X0, X1, ...; body digits on X1, X0, ...
-          NTT::template fwd3<0>(x, xch, tw, tid);
-        else
-          NTT::template fwd3<1>(x, xch, tw, tid);
+          for (int e = 0; e < E; ++e) d[e] = DG::get_int(pk[e], k);
+          if ((h ^ p) == 0)  // mask digits on X0, X1, ...; body digits on X1, X0, ...
+            NTT::template fwd3_small<0>(d, t0, x, xch, tw, tid);
+          else
+            NTT::template fwd3_small<1>(d, t0, x, xch, tw, tid);
+        } else {
+#pragma unroll
+          for (int e = 0; e < E; ++e) x[e] = DG::get(pk[e], k);
+          if ((h ^ p) == 0)
+            NTT::template fwd3<0>(x, xch, tw, tid);
+          else
+            NTT::template fwd3<1>(x, xch, tw, tid);
+        }
 #pragma unroll
         for (int e = 0; e < E; ++e) {
           accA[e] += mm<M>(x[e], (double)cur.a[e]);
@@ -294,10 +306,16 @@ __device__ __forceinline__ void cmux_step3(double (&acc0)[E], double (&acc1)[E],
     accA[e] = red<M>(accA[e]);
     accB[e] = red<M>(accB[e]);
   }
-  NTT::template inv3<1>(accA, xch, itw, tid);
+  if (OMR_NTT_SMALL0)
+    NTT::template inv3m<1>(accA, xch, tw, tid);
+  else
+    NTT::template inv3<1>(accA, xch, itw, tid);
 #pragma unroll
   for (int e = 0; e < E; ++e) acc0[e] = canon<M>(acc0[e] + accA[e]);
-  NTT::template inv3<0>(accB, xch, itw, tid);
+  if (OMR_NTT_SMALL0)
+    NTT::template inv3m<0>(accB, xch, tw, tid);
+  else
+    NTT::template inv3<0>(accB, xch, itw, tid);
 #pragma unroll
   for (int e = 0; e < E; ++e) acc1[e] = canon<M>(acc1[e] + accB[e]);
 }
@@ -649,20 +667,36 @@ __global__ __launch_bounds__(BR2_T, BR2_WAVES) void br2_trace_kernel(const uint3
   constexpr int T = BR2_T, E = BR2_E, N = N2;
   using NTT = WgNtt<M, T, E>;
   __shared__ double xch[OMR_XBUF3 ? NTT::LDS3_DOUBLES : (OMR_PAIR2 ? 2 : 1) * NTT::LDS_DOUBLES];
-  __shared__ double tws[2 * N];
+  // tw (N) + itw (N), or with OMR_NTT_SMALL0 tw (N) + the 129-entry stage-0 table
+  constexpr int TWS = (OMR_XBUF3 && OMR_NTT_SMALL0) ? N + 136 : 2 * N;
+  __shared__ double tws[TWS];
   const int tid = threadIdx.x;
   const size_t wg = blockIdx.x;
   const uint32_t *lwe = lwe_int + wg * (NI + 1);
   double acc0[E], acc1[E];
-  br_init<2, T, E>(acc0, acc1, tb.lut2, (int)lwe[NI], tws, tb.tw2, tb.itw2, tid);
-  const double *tw = tws, *itw = tws + N;
+  const double *tw = tws, *itw = tws + N, *t0 = tws + N;
+  if (OMR_XBUF3 && OMR_NTT_SMALL0) {
+    const int b = (int)lwe[NI];
+    const int rr = (2 * N - (b % (2 * N))) % (2 * N);
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int j = tid + e * T;
+      acc0[e] = 0.0;
+      acc1[e] = canon_small<M>(rot_read<N>(tb.lut2, j, rr));
+      tws[j] = tb.tw2[j];
+    }
+    if (tid <= 128) tws[N + tid] = canon<M>(mm<M>((double)(tid - 64), tb.tw2[1]));  // (d) * tw[1], d = tid - 64
+    __syncthreads();
+  } else {
+    br_init<2, T, E>(acc0, acc1, tb.lut2, (int)lwe[NI], tws, tb.tw2, tb.itw2, tid);
+  }
 #pragma unroll 1
   for (int i = 0; i < NI; ++i) {
     const int a = (int)__builtin_amdgcn_readfirstlane(lwe[i]) & (2 * N - 1);
     if (a == 0) continue;
 #if OMR_XBUF3
     cmux_step3<T, E, Key2T>(acc0, acc1, xch, a, bsk2 + (size_t)OMR_KEYROW2(i) * (2 * D2 * 2 * N), tw,
-                            itw, tid);
+                            itw, tid, t0);
 #elif OMR_PAIR2
     cmux_step_pair<2, T, E, LOGB2, D2, DROP2, Key2T, OMR_KEY_DEPTH2, false>(
         acc0, acc1, xch, a, bsk2 + (size_t)OMR_KEYROW2(i) * (2 * D2 * 2 * N), tw, itw, tid);
@@ -685,7 +719,15 @@ __global__ __launch_bounds__(BR2_T, BR2_WAVES) void br2_trace_kernel(const uint3
     return;
   }
   if (OMR_XBUF3) __syncthreads();  // the last inverse's cross-wave reads of X0 are done everywhere
-  hom_trace_store(acc0, acc1, xch, tw, itw, tk, tb, o, tid);
+  if (OMR_XBUF3 && OMR_NTT_SMALL0) {  // the trace's inverse table goes to the W buffer
+    double *itw_t = xch + 2 * N;
+#pragma unroll
+    for (int e = 0; e < E; ++e) itw_t[tid + e * T] = tb.itw2[tid + e * T];
+    __syncthreads();
+    hom_trace_store(acc0, acc1, xch, tw, itw_t, tk, tb, o, tid);
+  } else {
+    hom_trace_store(acc0, acc1, xch, tw, itw, tk, tb, o, tid);
+  }
 }
 
 }  // namespace omr

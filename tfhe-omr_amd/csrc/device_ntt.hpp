@@ -22,6 +22,9 @@
 #ifndef OMR_XBUF3
 #define OMR_XBUF3 1  // level-2 blind rotation: three-buffer exchanges, one barrier per transform
 #endif
+#ifndef OMR_NTT_SMALL0
+#define OMR_NTT_SMALL0 1  // level 2: inverse twiddles mirrored from the forward table, stage-0 digit table
+#endif
 #ifndef OMR_DB_XCH
 #define OMR_DB_XCH 1  // NTT exchanges through two alternating LDS buffers (fewer barriers)
 #endif
@@ -192,14 +195,14 @@ struct WgNtt {
   }
 
   // G: pass 0's twiddles (wave-uniform: hi == 0) come from the global table gtw by scalar loads
-  template <int P, int C, bool G = false>
+  template <int P, int C, bool G = false, int K0 = 0>
   __device__ static __forceinline__ void fwd_passC(double (&x)[C][E], const double *tw, int tid,
                                                    int &since_red, const double *__restrict__ gtw = nullptr) {
     constexpr int s0 = P * R;
     constexpr int r = (L - s0) < R ? (L - s0) : R;
     constexpr int lb = L - s0 - r;
 #pragma unroll
-    for (int k = 0; k < r; ++k) {
+    for (int k = K0; k < r; ++k) {
       if (since_red >= M::RED_FWD) {
 #pragma unroll
         for (int c = 0; c < C; ++c) reduce_all(x[c]);
@@ -231,7 +234,10 @@ struct WgNtt {
     }
   }
 
-  template <int P, int C, bool G = false>
+  // MIRROR: itw is the FORWARD table: psi^-brv(2^s + j) = -psi^brv(2^(s+1) - 1 - j) (the node's
+  // mirror in its stage), so w = tw[2^(s+1) - 1 - node] and the butterfly multiplies (v - u)
+  // instead of (u - v) -- the same exact product, and no inverse table in LDS.
+  template <int P, int C, bool G = false, bool MIRROR = false>
   __device__ static __forceinline__ void inv_passC(double (&x)[C][E], const double *itw, int tid,
                                                    int &since_red, const double *__restrict__ gitw = nullptr) {
     constexpr int s0 = P * R;
@@ -255,15 +261,16 @@ struct WgNtt {
 #ifdef OMR_EXPT_NTT_TW_CONST  // timing experiment only (wrong results)
         const double w = 7654321.0 + s * 3 + e;
 #else
+        const int node = (hi << k) | (ep >> (r - k));
         const double w = (P == 0 && G) ? gitw[(1 << s) + (ep >> (r - k))]
-                                       : itw[(1 << s) + ((hi << k) | (ep >> (r - k)))];
+                                       : (MIRROR ? itw[(2 << s) - 1 - node] : itw[(1 << s) + node]);
 #endif
 #pragma unroll
         for (int c = 0; c < C; ++c) {
           const double u = x[c][e];
           const double v = x[c][e + half];
           x[c][e] = u + v;
-          x[c][e + half] = mm<M>(u - v, w);
+          x[c][e + half] = MIRROR ? mm<M>(v - u, w) : mm<M>(u - v, w);
         }
       }
       ++since_red;
@@ -361,14 +368,38 @@ struct WgNtt {
       fwd3_from<P + 1, XB>(x, lds, tw, tid, since_red);
     }
   }
-  template <int P, int XB>
+  template <int P, int XB, bool MIRROR = false>
   __device__ static __forceinline__ void inv3_from(double (&x)[E], double *lds, const double *itw,
                                                    int tid, int &since_red) {
     if constexpr (P >= 0) {
       if constexpr (P < NPASS - 1) exchange3<P + 1, P, XB>(x, lds, tid);
-      inv_passC<P, 1>(reinterpret_cast<double(&)[1][E]>(x), itw, tid, since_red);
-      inv3_from<P - 1, XB>(x, lds, itw, tid, since_red);
+      inv_passC<P, 1, false, MIRROR>(reinterpret_cast<double(&)[1][E]>(x), itw, tid, since_red);
+      inv3_from<P - 1, XB, MIRROR>(x, lds, itw, tid, since_red);
     }
+  }
+  // Forward transform of a polynomial of small integer digits |d| <= 64: stage 0 (pairs e,
+  // e + E/2, twiddle tw[1] for every thread) takes d * tw[1] mod q from the 129-entry table t0
+  // (t0[d + 64], centred) instead of a modular product.
+  template <int XB>
+  __device__ static __forceinline__ void fwd3_small(const int (&d)[E], const double *t0, double (&x)[E],
+                                                    double *lds, const double *tw, int tid) {
+    static_assert(R == 3 && T == (1 << (L - R)), "stage-0 table written for full radix-8 first passes");
+#pragma unroll
+    for (int e = 0; e < E / 2; ++e) {
+      const double u = (double)d[e], v = t0[d[e + E / 2] + 64];
+      x[e] = u + v;
+      x[e + E / 2] = u - v;
+    }
+    int since_red = 1;
+    fwd_passC<0, 1, false, 1>(reinterpret_cast<double(&)[1][E]>(x), tw, tid, since_red);
+    fwd3_from<1, XB>(x, lds, tw, tid, since_red);
+  }
+  // Inverse with the forward table mirrored (MIRROR in inv_passC): tw is the forward table.
+  template <int XB>
+  __device__ static __forceinline__ void inv3m(double (&x)[E], double *lds, const double *tw, int tid) {
+    static_assert(cross_wave_exchanges() == 1, "three-buffer scheme written for one cross-wave exchange");
+    int since_red = 0;
+    inv3_from<NPASS - 1, XB, true>(x, lds, tw, tid, since_red);
   }
   // XB: the cross-wave buffer (0 / 1) this transform's single cross-wave exchange uses
   template <int XB>
