@@ -60,3 +60,21 @@ def test_level1_unsigned_min_canon():
     y = np.minimum(y, (y - q) & 0xFFFFFFFF)
     got = y.astype(np.int64) - h
     assert np.array_equal(got, _centred(x, q))
+
+
+def test_inverse_twiddles_mirror_forward_table():
+    """device_ntt.hpp inv_passC<MIRROR>: psi^-brv(2^s + j) = -psi^brv(2^(s+1) - 1 - j) (mod q2) for
+    every node of the 2048-point negacyclic table (psi = 22^((q2-1)/4096), 11-bit reversal), so
+    the level-2 inverse reads the forward table and multiplies (v - u) instead of (u - v)."""
+    q, L = Q2, 11
+    psi = pow(22, (q - 1) // 4096, q)
+    assert pow(psi, 2048, q) == q - 1
+
+    def brv(k):
+        return int(format(k, f"0{L}b")[::-1], 2)
+
+    tw = [pow(psi, brv(k), q) for k in range(1 << L)]
+    for s in range(L):
+        for j in range(1 << s):
+            itw = pow(psi, (4096 - brv((1 << s) + j)) % 4096, q)
+            assert itw == (q - tw[(2 << s) - 1 - j]) % q
