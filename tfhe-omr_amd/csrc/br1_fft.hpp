@@ -143,7 +143,10 @@ __device__ __forceinline__ void br1f_digits(const int (&ac)[2][16], int *st, int
     for (int i = 0; i < 16; ++i)
       pk[p][i] = Lvl1Int::digits(
           Lvl1Int::canon(st[(base + acc_coef(0, i)) & (2 * N1 - 1)] - ac[p][i]));
-    wave_lds_sync();
+    if (OMR_FFT_POSTREAD_WAIT)
+      wave_lds_sync();
+    else
+      wave_lds_fence();  // the next poly's writes stay below these reads
   }
 }
 

@@ -37,6 +37,9 @@ namespace omr {
 #ifndef OMR_FFT_TW_PAIR
 #define OMR_FFT_TW_PAIR 1  // odd sibling nodes reuse the even node's twiddle (w_odd = i w_even)
 #endif
+#ifndef OMR_FFT_POSTREAD_WAIT
+#define OMR_FFT_POSTREAD_WAIT 0  // one-wave FFTs: lgkmcnt(0) after each exchange's reads (br1 +1.1 %: off)
+#endif
 #ifndef OMR_FFT_DB
 #define OMR_FFT_DB 1  // multi-wave FFTs: double-buffered, wave-local where the pass pair allows
 #endif
@@ -46,6 +49,11 @@ namespace omr {
 // lgkmcnt wait is only needed with OMR_WAVE_SYNC_WAIT (the conservative form).
 __device__ __forceinline__ void wave_lds_sync() {
   if (OMR_WAVE_SYNC_WAIT) __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+  __builtin_amdgcn_wave_barrier();
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+}
+// Compiler-only ordering of one wave's LDS accesses (its LDS operations complete in order).
+__device__ __forceinline__ void wave_lds_fence() {
   __builtin_amdgcn_wave_barrier();
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
 }
@@ -183,7 +191,14 @@ struct WgFft {
         xi[c][e] = v.y;
       }
     if constexpr (T <= 64) {
-      wave_lds_sync();
+      // the next exchange's writes must not move above these reads: a compiler fence suffices
+      // (one wave's LDS operations complete in order); OMR_FFT_POSTREAD_WAIT also waits for them
+      if (OMR_FFT_POSTREAD_WAIT) {
+        wave_lds_sync();
+      } else {
+        __builtin_amdgcn_wave_barrier();
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+      }
     } else if constexpr (LAST || !db) {
       if constexpr (!LAST && WL)
         wave_lds_sync();
