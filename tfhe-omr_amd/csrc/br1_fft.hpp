@@ -36,6 +36,9 @@ namespace omr {
 #define BR1F_BARRIERS 2  // workgroup barriers per staged key row (1: next row issued after the MAC barrier;
                          // exposes the row latency: 212 vs 199 ms at D = 4,096)
 #endif
+#ifndef BR1F_DMA_SPREAD
+#define BR1F_DMA_SPREAD 0  // next key row's LDS-DMA pieces one per FFT pass instead of back to back (same speed: off)
+#endif
 #ifndef BR1F_KBUF
 #define BR1F_KBUF 2  // staged key-row buffers: 2 (two barriers per row) or 3 (one; needs BR1F_WPG 8 to fit LDS)
 #endif
@@ -248,6 +251,14 @@ __device__ __forceinline__ void krow_issue(const double2 *__restrict__ row, doub
     __builtin_amdgcn_global_load_lds(src, buf + comp * Fft512::N + e * 64, 16, 0, 0);
   }
 }
+// one of this wave's KROW_INSTR pieces of a row (u < KROW_INSTR)
+__device__ __forceinline__ void krow_issue_piece(const double2 *__restrict__ row, double2 *buf, int lane,
+                                                 int wave, int u) {
+  const int ins = wave * KROW_INSTR + u;
+  const int comp = ins >> 3, e = ins & 7;
+  __builtin_amdgcn_global_load_lds(row + comp * Fft512::N + lane * 8 + e, buf + comp * Fft512::N + e * 64, 16,
+                                   0, 0);
+}
 __device__ __forceinline__ void vm_wait_row_in_flight() {  // s_waitcnt vmcnt(KROW_INSTR)
   __builtin_amdgcn_s_waitcnt((KROW_INSTR & 0xF) | ((KROW_INSTR >> 4) << 14) | (0x7 << 4) | (0xF << 8));
 }
@@ -291,7 +302,8 @@ __device__ __forceinline__ void br1f_step_lds(int (&ac)[RW][2][16], double2 *xch
       wg_barrier_lds();  // every wave has finished reading buffer (q + 1) & 1 (row q - 1)
 #endif
 #ifndef OMR_EXPT_NO_KSTAGE
-      if (more) krow_issue(bskf + (size_t)(q + 1) * KROW_SLOTS, kbuf + ((q + 1) & 1) * KROW_SLOTS, lane, wave);
+      if (!BR1F_DMA_SPREAD && more)
+        krow_issue(bskf + (size_t)(q + 1) * KROW_SLOTS, kbuf + ((q + 1) & 1) * KROW_SLOTS, lane, wave);
 #endif
 #endif
       double xr[RW][8], xi[RW][8];
@@ -302,7 +314,20 @@ __device__ __forceinline__ void br1f_step_lds(int (&ac)[RW][2][16], double2 *xch
           xr[r][e] = Lvl1Int::digit(pk[r][p][e], k);
           xi[r][e] = Lvl1Int::digit(pk[r][p][8 + e], k);
         }
-      F::fwd<RW, BR1F_GTW != 0>(xr, xi, xch, tws, lane, gtw);
+      if (BR1F_DMA_SPREAD && BR1F_KBUF == 2 && BR1F_BARRIERS == 2) {
+        // the next row's LDS-DMA pieces go out one per FFT pass, among VALU work (an issue
+        // there costs less than four back to back after the barrier); all are issued before
+        // the wait for row q below
+        const double2 *nrow = bskf + (size_t)(q + 1) * KROW_SLOTS;
+        double2 *nbuf = kbuf + ((q + 1) & 1) * KROW_SLOTS;
+        if (more) krow_issue_piece(nrow, nbuf, lane, wave, 0);
+        F::fwd_hooked<RW, BR1F_GTW != 0>(xr, xi, xch, tws, lane, gtw, [&](int pass) {
+          if (more && pass + 1 < KROW_INSTR) krow_issue_piece(nrow, nbuf, lane, wave, pass + 1);
+        });
+        static_assert(!BR1F_DMA_SPREAD || KROW_INSTR == Fft512::NPASS + 1, "one piece before the FFT, one per pass");
+      } else {
+        F::fwd<RW, BR1F_GTW != 0>(xr, xi, xch, tws, lane, gtw);
+      }
 #if BR1F_KBUF == 3
       // three staged rows, one barrier per row: row q landed (row q + 1 may stay in flight) in
       // every wave's share, and every wave is past its multiply-accumulate of row q - 1, so

@@ -299,6 +299,29 @@ struct WgFft {
     OMR_FFT_FWD_STEP(4)
 #undef OMR_FFT_FWD_STEP
   }
+  // Forward transform calling hook(p) after the compute of pass p (p = 0 .. NPASS - 1): lets a
+  // caller spread independent work (e.g. LDS-DMA issues) over the transform's VALU phases.
+  template <int C, bool G, class Hook>
+  __device__ static __forceinline__ void fwd_hooked(double (&xr)[C][E], double (&xi)[C][E], double2 *lds,
+                                                    const double2 *tws, int lane,
+                                                    const double2 *__restrict__ gtw, Hook &&hook) {
+    static_assert(NPASS <= 5, "unrolled for up to 5 passes");
+    fwd_pass<0, C, G>(xr, xi, tws, lane, gtw);
+    hook(0);
+#define OMR_FFT_FWD_STEP(P)                                                                   \
+  if constexpr (NPASS > P) {                                                                  \
+    constexpr int Q = NPASS > P ? P : 1;                                                      \
+    exchange<C, Q - 1, Q, Q - 1, Q == NPASS - 1, (Q >= 2) && wave_local(Q >= 2 ? Q - 2 : 0, Q - 1)>( \
+        xr, xi, lds, lane);                                                                   \
+    fwd_pass<(NPASS > P ? P : 0), C>(xr, xi, tws, lane);                                      \
+    hook(P);                                                                                  \
+  }
+    OMR_FFT_FWD_STEP(1)
+    OMR_FFT_FWD_STEP(2)
+    OMR_FFT_FWD_STEP(3)
+    OMR_FFT_FWD_STEP(4)
+#undef OMR_FFT_FWD_STEP
+  }
   template <int C, bool G = false>
   __device__ static __forceinline__ void inv(double (&xr)[C][E], double (&xi)[C][E], double2 *lds,
                                              const double2 *tws, int lane,
