@@ -62,6 +62,33 @@ def test_level1_unsigned_min_canon():
     assert np.array_equal(got, _centred(x, q))
 
 
+def test_level2_forward_ntt_bound_with_stage01_tables():
+    """device_ntt.hpp fwd3_small (OMR_NTT_T0 = 2): after stages 0 and 1 from the tables (each
+    entry canonical) |x| <= |d| + 3 (q - 1) / 2 <= 2q; stages 2..5 each add mm(x, w) with
+    |mm| <= (0.5 + A/5) q for |x| <= A q, and the reduction comes before stage 6. The largest
+    value must stay below 2^53 = 8q (q2 < 2^50); the mm bound itself is replayed in FP64."""
+    q = Q2
+    bound = 2.0
+    for _ in range(4):  # stages 2, 3, 4, 5
+        bound += 0.5 + bound / 5
+    assert bound * q < 2.0**53 and bound < 6.9
+    rng = np.random.default_rng(14)
+    n = 20_000
+    a = np.rint(rng.uniform(-bound, bound, n) * q)
+    a[:2] = (-np.floor(bound * q), np.floor(bound * q))
+    w = rng.integers(-(q - 1) // 2, (q - 1) // 2 + 1, n).astype(np.float64)
+    w[:2] = ((q - 1) // 2, (q - 1) // 2)
+    h = a * w                        # rounded product
+    qe = np.rint(h * (1.0 / q))      # rint(h * fl(1/q))
+    # l = fma(a, w, -h) and fma(-qe, q, h) are exact on the device; replay with Python ints
+    for x, y, hh, e in zip(a.astype(np.int64), w.astype(np.int64), h, qe):
+        x, y, hh, e = int(x), int(y), int(hh), int(e)
+        r = (hh - e * q) + (x * y - hh)
+        assert abs(hh - e * q) < 2**53 and abs(r) < 2**53
+        assert r % q == (x * y) % q
+        assert abs(r) <= (0.5 + bound / 5) * q
+
+
 def test_inverse_twiddles_mirror_forward_table():
     """device_ntt.hpp inv_passC<MIRROR>: psi^-brv(2^s + j) = -psi^brv(2^(s+1) - 1 - j) (mod q2) for
     every node of the 2048-point negacyclic table (psi = 22^((q2-1)/4096), 11-bit reversal), so

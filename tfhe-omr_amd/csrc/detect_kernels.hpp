@@ -668,7 +668,7 @@ __global__ __launch_bounds__(BR2_T, BR2_WAVES) void br2_trace_kernel(const uint3
   using NTT = WgNtt<M, T, E>;
   __shared__ double xch[OMR_XBUF3 ? NTT::LDS3_DOUBLES : (OMR_PAIR2 ? 2 : 1) * NTT::LDS_DOUBLES];
   // tw (N) + itw (N), or with OMR_NTT_SMALL0 tw (N) + the 129-entry stage-0 table
-  constexpr int TWS = (OMR_XBUF3 && OMR_NTT_SMALL0) ? N + 136 : 2 * N;
+  constexpr int TWS = (OMR_XBUF3 && OMR_NTT_SMALL0) ? N + 136 * OMR_NTT_T0_TABLES : 2 * N;
   __shared__ double tws[TWS];
   const int tid = threadIdx.x;
   const size_t wg = blockIdx.x;
@@ -685,7 +685,12 @@ __global__ __launch_bounds__(BR2_T, BR2_WAVES) void br2_trace_kernel(const uint3
       acc1[e] = canon_small<M>(rot_read<N>(tb.lut2, j, rr));
       tws[j] = tb.tw2[j];
     }
-    if (tid <= 128) tws[N + tid] = canon<M>(mm<M>((double)(tid - 64), tb.tw2[1]));  // (d) * tw[1], d = tid - 64
+    if (tid <= 128) {  // table k: d * c_k, d = tid - 64 (c = tw1 [, tw2, tw1 tw2, tw3, tw1 tw3])
+      const double w1 = tb.tw2[1], w2 = tb.tw2[2], w3 = tb.tw2[3];
+      const double c[5] = {w1, w2, canon<M>(mm<M>(w1, w2)), w3, canon<M>(mm<M>(w1, w3))};
+#pragma unroll
+      for (int k = 0; k < OMR_NTT_T0_TABLES; ++k) tws[N + 136 * k + tid] = canon<M>(mm<M>((double)(tid - 64), c[k]));
+    }
     __syncthreads();
   } else {
     br_init<2, T, E>(acc0, acc1, tb.lut2, (int)lwe[NI], tws, tb.tw2, tb.itw2, tid);

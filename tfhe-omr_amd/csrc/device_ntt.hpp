@@ -25,6 +25,15 @@
 #ifndef OMR_NTT_SMALL0
 #define OMR_NTT_SMALL0 1  // level 2: inverse twiddles mirrored from the forward table, stage-0 digit table
 #endif
+#ifndef OMR_NTT_T0
+#define OMR_NTT_T0 2  // small-digit level-2 NTTs: 2 stages 0 and 1 from five LDS tables (-1.4 %),
+                      // 1 stage-0 products d * tw[1] from one table, 0 computed (+2 %)
+#endif
+#if OMR_NTT_T0 == 2
+#define OMR_NTT_T0_TABLES 5
+#else
+#define OMR_NTT_T0_TABLES 1
+#endif
 #ifndef OMR_DB_XCH
 #define OMR_DB_XCH 1  // NTT exchanges through two alternating LDS buffers (fewer barriers)
 #endif
@@ -379,14 +388,40 @@ struct WgNtt {
   }
   // Forward transform of a polynomial of small integer digits |d| <= 64: stage 0 (pairs e,
   // e + E/2, twiddle tw[1] for every thread) takes d * tw[1] mod q from the 129-entry table t0
-  // (t0[d + 64], centred) instead of a modular product.
+  // (t0[d + 64], centred) instead of a modular product; with OMR_NTT_T0 = 2 stage 1 too.
   template <int XB>
   __device__ static __forceinline__ void fwd3_small(const int (&d)[E], const double *t0, double (&x)[E],
                                                     double *lds, const double *tw, int tid) {
     static_assert(R == 3 && T == (1 << (L - R)), "stage-0 table written for full radix-8 first passes");
+    if constexpr (OMR_NTT_T0 == 2) {
+      // stages 0 and 1 from five tables (t0 + 136 k: d * c_k for c = tw1, tw2, tw1 tw2, tw3,
+      // tw1 tw3). Stage 1 pairs (e, e + 2) with tw[2] (e = 0, 1) and tw[3] (e = 4, 5), so
+      // tw2 * x[2] = tw2 d2 + tw1 tw2 d6 and tw3 * x[6] = tw3 d2 - tw1 tw3 d6 are table sums.
+      // Bound: |x| <= 2q after stage 1 (1.7q with the products), 6.84q before the stage-6
+      // reduction: below 8q < 2^53 and inside mm's exact range.
+      const double *T1 = t0, *T2 = t0 + 136, *T3 = t0 + 272, *T4 = t0 + 408, *T5 = t0 + 544;
+      const double a4 = T1[d[4] + 64], a5 = T1[d[5] + 64];
+      const double x0 = (double)d[0] + a4, x4 = (double)d[0] - a4;
+      const double x1 = (double)d[1] + a5, x5 = (double)d[1] - a5;
+      const double v0 = T2[d[2] + 64] + T3[d[6] + 64], v1 = T2[d[3] + 64] + T3[d[7] + 64];
+      const double v4 = T4[d[2] + 64] - T5[d[6] + 64], v5 = T4[d[3] + 64] - T5[d[7] + 64];
+      x[0] = x0 + v0;
+      x[2] = x0 - v0;
+      x[1] = x1 + v1;
+      x[3] = x1 - v1;
+      x[4] = x4 + v4;
+      x[6] = x4 - v4;
+      x[5] = x5 + v5;
+      x[7] = x5 - v5;
+      int since_red = 2;
+      fwd_passC<0, 1, false, 2>(reinterpret_cast<double(&)[1][E]>(x), tw, tid, since_red);
+      fwd3_from<1, XB>(x, lds, tw, tid, since_red);
+      return;
+    }
 #pragma unroll
     for (int e = 0; e < E / 2; ++e) {
-      const double u = (double)d[e], v = t0[d[e + E / 2] + 64];
+      const double u = (double)d[e];
+      const double v = OMR_NTT_T0 ? t0[d[e + E / 2] + 64] : mm<M>((double)d[e + E / 2], tw[1]);
       x[e] = u + v;
       x[e + E / 2] = u - v;
     }
