@@ -92,11 +92,12 @@ struct DigitsTrace {
       pk[k / 10] |= (uint32_t)((int)d + 2) << (3 * (k % 10));
     }
   }
-  __device__ static __forceinline__ double get(const uint32_t (&pk)[DW], int k) {
+  __device__ static __forceinline__ int get_int(const uint32_t (&pk)[DW], int k) {
     const int wi = k / 10;
     const uint32_t w = wi == 0 ? pk[0] : (wi == 1 ? pk[1] : pk[2]);
-    return (double)((int)((w >> (3 * (k - 10 * wi))) & 7u) - 2);
+    return (int)((w >> (3 * (k - 10 * wi))) & 7u) - 2;
   }
+  __device__ static __forceinline__ double get(const uint32_t (&pk)[DW], int k) { return (double)get_int(pk, k); }
 };
 
 // (X^r * p)[j] for p in LDS, r in [0, 2N): sign-corrected read.
@@ -653,6 +654,116 @@ __device__ __forceinline__ void hom_trace_store(double (&acc0)[BR2_E], double (&
   }
 }
 
+// One trace digit d on the three-buffer NTT (cross-wave buffer XB): forward transform of the
+// small digits (|d| <= 2, stage tables t0) and multiply-accumulate with the key row.
+template <int XB>
+__device__ __forceinline__ void trace_digit3(const uint32_t (&pk)[BR2_E][DigitsTrace::DW], int d,
+                                             const double *__restrict__ key, double (&accA)[BR2_E],
+                                             double (&accB)[BR2_E], double *xch, const double *tw,
+                                             const double *t0, int tid) {
+  using M = Mod<2>;
+  constexpr int T = BR2_T, E = BR2_E, N = N2;
+  using NTT = WgNtt<M, T, E>;
+  const double *ka = key + (size_t)(d * 2) * N + tid * E;  // alpha (pre-scaled by N^-1)
+  const double *kb = ka + N;                                 // beta (unscaled)
+  double kra[E], krb[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    kra[e] = ka[e];
+    krb[e] = kb[e];
+  }
+  int dg[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) dg[e] = DigitsTrace::get_int(pk[e], d);
+  double x[E];
+  NTT::template fwd3_small<XB>(dg, t0, x, xch, tw, tid);
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    accA[e] += mm<M>(x[e], kra[e]);
+    accB[e] += mm<M>(x[e], krb[e]);
+  }
+  if ((d % 3) == 2) {
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      accA[e] = red<M>(accA[e]);
+      accB[e] = red<M>(accB[e]);
+    }
+  }
+}
+
+// hom_trace_store on the three-buffer exchanges (OMR_TRACE3; xch holds 3N doubles, tw the
+// forward table, t0 the small-digit tables). Per automorphism step: staging of sigma_g(a)
+// through X0 (trailing barrier), the 25 digit transforms on X1, X0, ..., X1 (no trailing
+// barriers: consecutive cross-wave uses alternate), the body permutation through X0 (its last
+// use, digit 23, is behind digit 24's barrier; trailing barrier), the inverse on X1 with the
+// mirrored forward table (X1's last use, digit 24, is behind the permutation's barriers). The
+// next step's staging writes X0, whose last use had a trailing barrier.
+__device__ __forceinline__ void hom_trace_store3(double (&acc0)[BR2_E], double (&acc1)[BR2_E],
+                                                 double *xch, const double *tw, const double *t0,
+                                                 const double *__restrict__ tk, const DeviceTables &tb,
+                                                 uint64_t *__restrict__ o, int tid) {
+  using M = Mod<2>;
+  constexpr int T = BR2_T, E = BR2_E, N = N2;
+  using NTT = WgNtt<M, T, E>;
+  static_assert(DT % 2 == 1, "digit pairs on X1, X0 and a last digit on X1");
+  constexpr double NINV = -549755813880.0;  // 2048^-1 mod q2, centred (secret.rs:167-168)
+  double ca[E], cb[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    ca[e] = canon<M>(mm<M>(acc0[e], NINV));
+    cb[e] = canon<M>(mm<M>(acc1[e], NINV));
+  }
+  NTT::fwd(cb, xch, tw, tid);  // X0, X1 (double-buffered), trailing barrier
+#pragma unroll
+  for (int e = 0; e < E; ++e) cb[e] = canon<M>(cb[e]);
+#pragma unroll 1
+  for (int k = 0; k < TRACE_STEPS; ++k) {
+    const uint16_t *src = tb.trace_src + k * N;
+    const uint16_t *perm = tb.trace_perm + k * N;
+    uint32_t pk[E][DigitsTrace::DW];
+#pragma unroll
+    for (int e = 0; e < E; ++e) xch[tid + e * T] = ca[e];
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int s = src[tid + e * T];
+      DigitsTrace::pack(s < N ? xch[s] : -xch[s - N], pk[e]);  // sigma_g(a)
+    }
+    __syncthreads();
+    double accA[E], accB[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) accA[e] = accB[e] = 0.0;
+    const double *key = tk + (size_t)k * DT * 2 * N;
+#pragma unroll 1
+    for (int d = 0; d < DT - 1; d += 2) {
+      trace_digit3<1>(pk, d, key, accA, accB, xch, tw, t0, tid);
+      trace_digit3<0>(pk, d + 1, key, accA, accB, xch, tw, t0, tid);
+    }
+    trace_digit3<1>(pk, DT - 1, key, accA, accB, xch, tw, t0, tid);
+    // b_ntt += sigma_g(b)_ntt + B
+#pragma unroll
+    for (int e = 0; e < E; ++e) xch[tid * E + e] = cb[e];
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < E; ++e) cb[e] = canon<M>(cb[e] + xch[perm[tid * E + e]] + red<M>(accB[e]));
+    __syncthreads();
+    // a += INTT(A)
+#pragma unroll
+    for (int e = 0; e < E; ++e) accA[e] = red<M>(accA[e]);
+    NTT::template inv3m<1>(accA, xch, tw, tid);
+#pragma unroll
+    for (int e = 0; e < E; ++e) ca[e] = canon<M>(ca[e] + accA[e]);
+  }
+  __syncthreads();  // the last inverse's cross-wave reads of X1 are done everywhere
+  NTT::fwd(ca, xch, tw, tid);
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int t = tid * E + e;
+    o[t] = to_u64<M>(canon<M>(ca[e]));
+    o[N + t] = to_u64<M>(cb[e]);
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // Level 2 (second_level_bootstrapping, detector.rs:599-624) fused with hom_trace (:626-639):
 // one workgroup per message. mode 0: trace + NTT output u64 [wg][2][N2] (NttRlweCiphertext);
@@ -724,7 +835,9 @@ __global__ __launch_bounds__(BR2_T, BR2_WAVES) void br2_trace_kernel(const uint3
     return;
   }
   if (OMR_XBUF3) __syncthreads();  // the last inverse's cross-wave reads of X0 are done everywhere
-  if (OMR_XBUF3 && OMR_NTT_SMALL0) {  // the trace's inverse table goes to the W buffer
+  if (OMR_XBUF3 && OMR_NTT_SMALL0 && OMR_TRACE3) {
+    hom_trace_store3(acc0, acc1, xch, tw, t0, tk, tb, o, tid);
+  } else if (OMR_XBUF3 && OMR_NTT_SMALL0) {  // the trace's inverse table goes to the W buffer
     double *itw_t = xch + 2 * N;
 #pragma unroll
     for (int e = 0; e < E; ++e) itw_t[tid + e * T] = tb.itw2[tid + e * T];

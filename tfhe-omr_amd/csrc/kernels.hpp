@@ -67,6 +67,10 @@ namespace omr {
 #ifndef OMR_BR2_PERSIST
 #define OMR_BR2_PERSIST 0 // level 2: resident-sized grid walking messages with a grid stride
 #endif
+#ifndef OMR_TRACE3
+#define OMR_TRACE3 0      // trace digit transforms on the three-buffer NTT with the small-digit tables
+                          // (bit-exact; 128 B/lane of scratch in the fused kernel: br2 +1 %, off)
+#endif
 #ifndef OMR_KEY_NT
 #define OMR_KEY_NT 0
 #endif
