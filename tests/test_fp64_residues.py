@@ -89,6 +89,20 @@ def test_level2_forward_ntt_bound_with_stage01_tables():
         assert abs(r) <= (0.5 + bound / 5) * q
 
 
+def test_level2_mac_four_products_per_reduction():
+    """detect_kernels.hpp cmux_step3 (OMR_MAC_RED4): the forward transform ends 5 stages after
+    its reduction (|x| <= q/2 + 2 there), so |x| <= 4.96q; with |key| <= q/2 each product
+    |mm(x, key)| <= (0.5 + 4.96/5) q, and a reduced sum (|acc| <= q/2 + 2) plus four products
+    stays below 8q < 2^53. A fifth product would not fit."""
+    b = 0.5
+    for _ in range(5):  # stages 6..10
+        b += 0.5 + b / 5
+    assert 4.9 < b < 4.97
+    prod = 0.5 + b / 5
+    assert 0.5 + 4 * prod < 6.5 and (0.5 + 4 * prod) * Q2 < 2.0**53
+    assert (0.5 + 5 * prod) * Q2 > 2.0**53 * 0.99  # no margin for five
+
+
 def test_inverse_twiddles_mirror_forward_table():
     """device_ntt.hpp inv_passC<MIRROR>: psi^-brv(2^s + j) = -psi^brv(2^(s+1) - 1 - j) (mod q2) for
     every node of the 2048-point negacyclic table (psi = 22^((q2-1)/4096), 11-bit reversal), so

@@ -291,7 +291,9 @@ __device__ __forceinline__ void cmux_step3(double (&acc0)[E], double (&acc1)[E],
           accA[e] += mm<M>(x[e], (double)cur.a[e]);
           accB[e] += mm<M>(x[e], (double)cur.b[e]);
         }
-        if ((k % 3) == 2) {
+        // |x| <= 4.96q after the transform, so |mm(x, key)| <= 1.49q: four products on a
+        // reduced sum stay below 6.5q < 2^53 (OMR_MAC_RED4); three with the per-row rule
+        if (OMR_MAC_RED4 ? ((r % 4) == 3 && r + 1 < 2 * D2) : (k % 3) == 2) {
 #pragma unroll
           for (int e = 0; e < E; ++e) {
             accA[e] = red<M>(accA[e]);

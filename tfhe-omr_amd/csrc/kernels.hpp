@@ -71,6 +71,9 @@ namespace omr {
 #define OMR_TRACE3 0      // trace digit transforms on the three-buffer NTT with the small-digit tables
                           // (bit-exact; 128 B/lane of scratch in the fused kernel: br2 +1 %, off)
 #endif
+#ifndef OMR_MAC_RED4
+#define OMR_MAC_RED4 1    // level-2 CMUX: reduce the NTT-domain accumulators every 4 digit products
+#endif
 #ifndef OMR_KEY_NT
 #define OMR_KEY_NT 0
 #endif
