@@ -42,6 +42,10 @@ namespace omr {
 #ifndef BR1F_KBUF
 #define BR1F_KBUF 2  // staged key-row buffers: 2 (two barriers per row) or 3 (one; needs BR1F_WPG 8 to fit LDS)
 #endif
+#ifndef BR1F_T0
+#define BR1F_T0 0  // stage 0 of the digit FFTs (one uniform twiddle w) from a 33-entry LDS table d * w
+                   // (bit-exact; 730 vs 705 ms: the table reads cost more than the VALU saved, off)
+#endif
 #ifndef BR1F_DIGIT_SBFE
 #define BR1F_DIGIT_SBFE 2  // digit words in two's-complement fields; 2: two uniform shifts per digit, 1: v_bfe_i32 (inline asm, slower)
 #endif
@@ -91,6 +95,12 @@ struct Lvl1Int {
     u = u < 0 ? u + N1 : u;
     const int v = p[u];
     return neg ? -v : v;
+  }
+  // signed digit k of a digits() word as an int (two-shift form)
+  __device__ static __forceinline__ int digit_int(uint32_t w, int k) {
+    static_assert(BR1F_DIGIT_SBFE == 2, "integer digits written for the two-shift form");
+    const int s1 = k < D1 - 1 ? 32 - LOGB1 * (k + 1) : 0, s2 = k < D1 - 1 ? 32 - LOGB1 : LOGB1 * (D1 - 1);
+    return (int)(w << s1) >> s2;
   }
   // signed digit k of a digits() word
   __device__ static __forceinline__ double digit(uint32_t w, int k) {
@@ -279,7 +289,7 @@ template <int RW>
 __device__ __forceinline__ void br1f_step_lds(int (&ac)[RW][2][16], double2 *xch, const double2 *tws,
                                               const int (&a)[RW], const double2 *__restrict__ bskf,
                                               int q0, int qtotal, double2 *kbuf, int lane, int wave,
-                                              const double2 *__restrict__ gtw) {
+                                              const double2 *__restrict__ gtw, const double2 *t1) {
   using F = Fft512;
   uint32_t pk[RW][2][16];
 #pragma unroll
@@ -307,13 +317,33 @@ __device__ __forceinline__ void br1f_step_lds(int (&ac)[RW][2][16], double2 *xch
 #endif
 #endif
       double xr[RW][8], xi[RW][8];
+      if (BR1F_T0) {
+        // stage 0 pairs (e, e + 4) under the one twiddle w = tw[1]: w * x[e + 4] for the small
+        // digits (|d| <= 16) is a sum of table entries t1[d + 16] = (d w.x, d w.y); rounded
+        // products instead of an fma, inside the FFT's error budget (tools/fft_exactness.py
+        // models unfused complex products everywhere)
 #pragma unroll
-      for (int r = 0; r < RW; ++r)
+        for (int r = 0; r < RW; ++r)
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          xr[r][e] = Lvl1Int::digit(pk[r][p][e], k);
-          xi[r][e] = Lvl1Int::digit(pk[r][p][8 + e], k);
-        }
+          for (int e = 0; e < 4; ++e) {
+            const double2 a = t1[Lvl1Int::digit_int(pk[r][p][e + 4], k) + 16];
+            const double2 b = t1[Lvl1Int::digit_int(pk[r][p][8 + e + 4], k) + 16];
+            const double vr = a.x - b.y, vi = a.y + b.x;
+            const double ur = Lvl1Int::digit(pk[r][p][e], k), ui = Lvl1Int::digit(pk[r][p][8 + e], k);
+            xr[r][e] = ur + vr;
+            xi[r][e] = ui + vi;
+            xr[r][e + 4] = ur - vr;
+            xi[r][e + 4] = ui - vi;
+          }
+      } else {
+#pragma unroll
+        for (int r = 0; r < RW; ++r)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            xr[r][e] = Lvl1Int::digit(pk[r][p][e], k);
+            xi[r][e] = Lvl1Int::digit(pk[r][p][8 + e], k);
+          }
+      }
       if (BR1F_DMA_SPREAD && BR1F_KBUF == 2 && BR1F_BARRIERS == 2) {
         // the next row's LDS-DMA pieces go out one per FFT pass, among VALU work (an issue
         // there costs less than four back to back after the barrier); all are issued before
@@ -325,8 +355,9 @@ __device__ __forceinline__ void br1f_step_lds(int (&ac)[RW][2][16], double2 *xch
           if (more && pass + 1 < KROW_INSTR) krow_issue_piece(nrow, nbuf, lane, wave, pass + 1);
         });
         static_assert(!BR1F_DMA_SPREAD || KROW_INSTR == Fft512::NPASS + 1, "one piece before the FFT, one per pass");
+        static_assert(!BR1F_DMA_SPREAD || !BR1F_T0, "the hooked transform starts at stage 0");
       } else {
-        F::fwd<RW, BR1F_GTW != 0>(xr, xi, xch, tws, lane, gtw);
+        F::fwd<RW, BR1F_GTW != 0, BR1F_T0 ? 1 : 0>(xr, xi, xch, tws, lane, gtw);
       }
 #if BR1F_KBUF == 3
       // three staged rows, one barrier per row: row q landed (row q + 1 may stay in flight) in
@@ -395,6 +426,7 @@ __global__ __launch_bounds__(64 * BR1F_WPG, BR1F_WAVES) void br1f_kernel(
   constexpr int NF = Fft512::N, W = BR1F_WPG;
   __shared__ double2 xch_all[W][RW * Fft512::BUF];
   __shared__ double2 tws[NF];
+  __shared__ double2 t1tab[BR1F_T0 ? 33 : 1];
   __shared__ uint16_t la_all[W][RW][N0];
 #if BR1F_KEY_LDS
   static_assert(16 % W == 0, "LDS key staging: W divides the row's 16 one-KiB pieces");
@@ -433,6 +465,11 @@ __global__ __launch_bounds__(64 * BR1F_WPG, BR1F_WAVES) void br1f_kernel(
     }
   }
   for (int j = threadIdx.x; j < NF; j += 64 * W) tws[j] = tb.fft1[j];
+  if (BR1F_T0 && threadIdx.x < 33) {  // d * w for d = -16 .. 16, w = the stage-0 twiddle
+    const double2 w = tb.fft1[1];
+    const double d = (double)((int)threadIdx.x - 16);
+    t1tab[threadIdx.x] = make_double2(d * w.x, d * w.y);
+  }
   __syncthreads();
 #if BR1F_KEY_LDS
   // every step runs (a = 0 gives zero digits and leaves ACC unchanged) so the waves share the
@@ -444,7 +481,7 @@ __global__ __launch_bounds__(64 * BR1F_WPG, BR1F_WAVES) void br1f_kernel(
     int a[RW];
 #pragma unroll
     for (int r = 0; r < RW; ++r) a[r] = __builtin_amdgcn_readfirstlane(la[r][i]);
-    br1f_step_lds<RW>(ac, xch, tws, a, bskf, i * 2 * D1, N0 * 2 * D1, kbuf, lane, wave, tb.fft1);
+    br1f_step_lds<RW>(ac, xch, tws, a, bskf, i * 2 * D1, N0 * 2 * D1, kbuf, lane, wave, tb.fft1, t1tab);
   }
   __syncthreads();
 #else

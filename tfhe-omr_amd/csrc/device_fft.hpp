@@ -220,13 +220,14 @@ struct WgFft {
     return tws[twiddle_index<P>(k, e, lane)];
   }
 
-  template <int P, int C, bool G = false>
+  // K0: first stage of the pass (a caller that computed stage 0 itself passes 1)
+  template <int P, int C, bool G = false, int K0 = 0>
   __device__ static __forceinline__ void fwd_pass(double (&xr)[C][E], double (&xi)[C][E],
                                                   const double2 *tws, int lane,
                                                   const double2 *__restrict__ gtw = nullptr) {
     constexpr int r = stages(P);
 #pragma unroll
-    for (int k = 0; k < r; ++k) {
+    for (int k = K0; k < r; ++k) {
       const int half = 1 << (r - 1 - k);
 #pragma unroll
       for (int e = 0; e < E; ++e) {
@@ -280,12 +281,12 @@ struct WgFft {
   }
   // C transforms at once (lds holds C * BUF complex)
   // G: pass-0 twiddles from the global table gtw (must be non-null)
-  template <int C, bool G = false>
+  template <int C, bool G = false, int K0 = 0>
   __device__ static __forceinline__ void fwd(double (&xr)[C][E], double (&xi)[C][E], double2 *lds,
                                              const double2 *tws, int lane,
                                              const double2 *__restrict__ gtw = nullptr) {
     static_assert(NPASS <= 5, "unrolled for up to 5 passes");
-    fwd_pass<0, C, G>(xr, xi, tws, lane, gtw);
+    fwd_pass<0, C, G, K0>(xr, xi, tws, lane, gtw);
 #define OMR_FFT_FWD_STEP(P)                                                                   \
   if constexpr (NPASS > P) {                                                                  \
     constexpr int Q = NPASS > P ? P : 1;                                                      \
