@@ -22,7 +22,7 @@ for f in sorted(glob.glob(f"{d}/pmc*/pmc_counter_collection.csv")):
         if (k, r.get("Dispatch_Id", r.get("Correlation_Id"))) not in seen and c == ctrs[0]:
             seen.add((k, r.get("Dispatch_Id", r.get("Correlation_Id"))))
             launches[k] = launches.get(k, 0) + 1
-out = {"source": d, "messages_per_launch": msgs, "lanes": 64, "kernels": {}}
+out = {"source": f"profiles/<tag>/compute_summary.json from {d}", "messages_per_launch": msgs, "lanes": 64, "kernels": {}}
 for k, c in agg.items():
     if not all(x in c for x in ctrs[:4]):
         continue
