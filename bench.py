@@ -1,19 +1,22 @@
 """bench.py — detect-phase messages/s of the MI355X InstantOMR detector.
 
-Workload (BASELINE.json configs[2]): full Detector::detect() (detector.rs:135-166) over
-D = 65,536 synthetic clues per GPU (50 pertinent, the rest from a second sender key),
-inputs resident in HBM, outputs (the pertinency vector, D x 32 KiB) written to HBM.
-One step = one detect pass over the D clues of every rank. N > 1: one process per GPU
-(torch.distributed, RCCL), each rank owns a contiguous range of global message indices
-(weak scaling, no data-path collective). Rank 0 prints one JSON line.
+Workload: full Detector::detect() (detector.rs:135-166) over synthetic clues (50 pertinent over
+the whole job, the rest from a second sender key), inputs resident in HBM, outputs (the
+pertinency vector, D x 32 KiB) written to HBM. One step = one detect pass over the clues of
+every rank. One process per GPU (torch.distributed, RCCL); each rank owns a contiguous range of
+global message indices and detect needs no collective.
+  weak scaling (default):  --messages D per GPU (65,536: BASELINE configs[2] at N = 1,
+                           configs[3]'s D = 524,288 at N = 8)
+  strong scaling:          --total-messages T split over the N GPUs (T = 524,288: configs[3]'s
+                           1/2/4/8-GPU curve; T = 2^20: configs[4])
 
-After the timed detect steps, one end-to-end pass (configs[4] shape) runs
-on the last pertinency vector: encode_pertinent_indices + encode_pertinent_payloads over each
-rank's shard with global indices, one RCCL reduce of the partial digests to rank 0, and the
-client-side retrieval (the library's Retriever) must recover exactly the pertinent indices and
-their payloads ("e2e" in the JSON line; --no-e2e skips it).
+After the timed detect steps, one end-to-end pass (omr_dist.encode_and_reduce, the code path the
+gloo test drives) runs on the last pertinency vector: encode_pertinent_indices +
+encode_pertinent_payloads over each rank's shard with global indices, one RCCL reduce of the
+partial digests to rank 0, and the client-side retrieval (the library's Retriever) must recover
+exactly the pertinent indices and their payloads ("e2e"; --no-e2e skips it).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--messages D] [--no-e2e]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--messages D | --total-messages T]
 """
 from __future__ import annotations
 
@@ -29,6 +32,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "tfhe-omr_amd"))
 
 import omr_amd as A  # noqa: E402
+import omr_dist  # noqa: E402
 
 # Algorithmic bytes per message (SURVEY.md §8d key-streaming model, reference u32/u64 formats):
 # every evaluation-key element counted once per use by one message.
@@ -44,10 +48,13 @@ KERNEL_BYTES = {  # per message, per pipeline stage (kernel names from A.detect_
     "br2": BR2_BYTES + TRACE_BYTES + 671 * 4 + 2 * 2048 * 8,
 }
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
-# FP64 VALU issue rate: 256 CUs x 4 SIMDs x 16 FP64 lanes x 2.4 GHz (78.6 TFLOP/s counting FMA as
-# 2); the arithmetic microbenchmark reaches 95 % of it (profiles/r01_microbench_arith.txt).
-FP64_PEAK_T_LANE_INSTR = 256 * 4 * 16 * 2.4e9 / 1e12
-PUBLISHED_CPU_MSG_S = 1e3 / 234.073003  # README.md:122, 1 thread AVX-512
+# FP64 VALU peak: 256 CUs x 4 SIMDs x 16 FP64 FMA lanes x 2 FLOP x 2.4 GHz = 78.6 TFLOP/s (a wave64
+# FP64 instruction issues in 4 cycles); the arithmetic microbenchmark reaches 95 % of it
+# (profiles/r01_microbench_arith.txt).
+FP64_PEAK_TFLOPS = 256 * 4 * 16 * 2 * 2.4e9 / 1e12
+PUBLISHED_CPU_MS_PER_MSG = 234.073003  # README.md:122, 1 thread, AVX-512 CPU (model not stated)
+WEIGHT_SEED = bytes(range(1, 33))
+INDEX_SEED = 9
 
 
 def parse():
@@ -55,9 +62,13 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--messages", type=int, default=65536, help="clues per GPU")
+    g = ap.add_mutually_exclusive_group()
+    g.add_argument("--messages", type=int, default=None, help="clues per GPU (weak scaling; default 65,536)")
+    g.add_argument("--total-messages", type=int, default=None, help="clues over all GPUs (strong scaling)")
+    ap.add_argument("--batch", type=int, default=16384, help="messages per detect chunk (omr_ctx_set_batch)")
     ap.add_argument("--pertinent", type=int, default=50)
-    ap.add_argument("--cpu-baseline-msgs", type=int, default=256)
+    ap.add_argument("--cpu-single-msgs", type=int, default=8, help="CPU baseline: 1-thread sample")
+    ap.add_argument("--cpu-msgs-per-thread", type=int, default=4, help="CPU baseline: all-core sample per thread")
     ap.add_argument("--force-dist", action="store_true",
                     help="initialise the RCCL process group even at world size 1 (rehearses the N > 1 path)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -66,31 +77,70 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(dk, ca, cb, nmsg):
-    """The oracle detect() (oracle/, plain-C restatement of the reference path: kind "port")
-    timed on this host's cores over a bounded sample (the Rust reference cannot be built
-    here). Test infrastructure, used only for this reported leg."""
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_threads() -> int:
+    """Host threads this process may use: its CPU affinity, capped by OMP_NUM_THREADS when set
+    (the GPU box exports the box's CPU share there; os.cpu_count() shows the whole machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    env = os.environ.get("OMP_NUM_THREADS", "")
+    return max(1, min(n, int(env))) if env.isdigit() and int(env) > 0 else n
+
+
+def cpu_baseline(dk, ca, cb, single_msgs, per_thread):
+    """The oracle detect() (oracle/, plain-C restatement of the reference path: kind "port") timed
+    on this host (the Rust reference cannot be built here), per BASELINE.md §3:
+    (i) 1 thread, mean over `single_msgs` messages; (ii) every usable core, one message per
+    thread at a time like rayon, over per_thread x cores messages. Test infrastructure, used only
+    for this reported leg, after the timed GPU region."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib as O
 
-    cores = min(16, os.cpu_count() or 1)
+    cores = cpu_threads()
+    n_all = per_thread * cores
+    if ca.shape[0] < max(single_msgs, n_all):
+        raise ValueError("not enough clues for the CPU baseline sample")
     det = O.OracleDetector(dk.bsk1, dk.ksk, dk.bsk2, dk.trace_key)
     det.detect_batch(ca[:1], cb[:1], nthreads=1)  # warm the tables
     t = time.perf_counter()
-    det.detect_batch(ca[:nmsg], cb[:nmsg], nthreads=cores)
-    dt = time.perf_counter() - t
+    det.detect_batch(ca[:single_msgs], cb[:single_msgs], nthreads=1)
+    t1 = time.perf_counter() - t
+    t = time.perf_counter()
+    det.detect_batch(ca[:n_all], cb[:n_all], nthreads=cores)
+    tn = time.perf_counter() - t
     det.close()
-    return {"value": round(nmsg / dt, 3), "unit": "messages/s", "cores": cores, "kind": "port",
-            "sample": f"{nmsg} detect() calls of the same workload, OpenMP over messages, {dt:.1f}s wall"}
+    return {"value": round(n_all / tn, 3), "unit": "messages/s", "cores": cores, "kind": "port",
+            "sample": (f"{n_all} detect() calls ({per_thread} per thread) on {cores} threads, OpenMP over "
+                       f"messages, {tn:.1f} s wall; 1 thread: {single_msgs} calls, {t1:.1f} s"),
+            "single_thread_ms_per_msg": round(t1 / single_msgs * 1e3, 2),
+            "all_cores_msgs_per_s": round(n_all / tn, 3),
+            "nproc": os.cpu_count(), "cpu_model": cpu_model(),
+            "published_reference_ms_per_msg": PUBLISHED_CPU_MS_PER_MSG,
+            "published_reference_note": "reference Rust detect(), 1 thread, AVX-512, different machine "
+                                        "(README.md:122)"}
 
 
-def workload_name(D, world):
-    """BASELINE.json config the run corresponds to (configs[2] at D = 65,536 per GPU, configs[3]
-    at N = 8, configs[4]'s detect + encode shape at D = 2^20 over the job)."""
-    name = f"full detect() D={D} per GPU, {D * world} total"
-    if D == 65536:
-        name += " (configs[2]; configs[3] at N=8)"
-    elif D * world == 1 << 20:
+def workload_name(per_rank, total, world, strong):
+    if strong:
+        name = f"full detect() D={total} sharded over {world} GPU(s) (strong scaling)"
+        if total == 524288:
+            name += " (configs[3])"
+        elif total == 1 << 20:
+            name += " (configs[4]: detect + encode + retrieval at D=2^20)"
+        return name
+    name = f"full detect() D={per_rank} per GPU, {total} total (weak scaling)"
+    if per_rank == 65536:
+        name += " (configs[2] at N=1; configs[3]'s D=524,288 at N=8)"
+    elif total == 1 << 20:
         name += " (configs[4]: detect + encode + retrieval at D=2^20)"
     return name
 
@@ -114,49 +164,36 @@ def synthetic_payloads(first: int, count: int) -> np.ndarray:
     return ((h >> np.uint64(24)) & np.uint64(255)).astype(np.uint16)
 
 
-def end_to_end(det, pack_a, d_out, D, first, total, pert, dist, dev, stream, rank):
-    """encode_pertinent_indices + encode_pertinent_payloads over this shard (global indices),
-    one RCCL reduce to rank 0, then Retriever::decode_digest on rank 0 (examples/omr.rs:219-293)."""
-    import torch
-
-    rp = A.RetrievalParams(total, len(pert))
-    n_idx, n_pay, per = rp.max_encode_indices_cipher_count, rp.cmb_cipher_count, rp.cmb_count_per_cipher
-    seed = bytes(range(1, 33))
-    d_pay = torch.from_numpy(synthetic_payloads(first, D).view(np.int16)).to(dev)
-    d_w = torch.from_numpy(A.payload_weights(seed, rp).view(np.int16)).to(dev)
-    d_dig = torch.empty((n_idx + n_pay, 2, 2048), dtype=torch.int64, device=dev)
-    torch.cuda.synchronize(dev)
-    if dist:
-        dist.barrier()
-    t0 = time.perf_counter()
-    det.encode_indices_device(d_out.data_ptr(), D, first, total, 9, 0, n_idx, d_dig.data_ptr(), stream.cuda_stream)
-    det.encode_payloads_device(d_out.data_ptr(), d_pay.data_ptr(), D, first, total, d_w.data_ptr(), n_pay, per,
-                               d_dig[n_idx:].data_ptr(), stream.cuda_stream)
-    torch.cuda.synchronize(dev)
-    t1 = time.perf_counter()
-    if dist:
-        dist.reduce(d_dig, dst=0, op=dist.ReduceOp.SUM)  # partial digests (< q2 each), int64 sum
-        torch.cuda.synchronize(dev)
-    t2 = time.perf_counter()
-    times = [t1 - t0, t2 - t0]
-    if dist:
-        tt = torch.tensor(times, dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        times = tt.tolist()
-    if rank != 0:
-        return None
-    digest = d_dig.cpu().numpy().view(np.uint64) % np.uint64(A.Q2)
-    t3 = time.perf_counter()
-    indices, pays = A.Retriever(rp, pack_a).decode_digest(digest[:n_idx], digest[n_idx:], seed)
-    t4 = time.perf_counter()
-    ok = indices == [int(v) for v in pert]
-    if ok:
-        want = np.concatenate([synthetic_payloads(int(i), 1) for i in indices]) if indices else np.zeros((0, 612))
-        ok = bool(np.array_equal(pays, want))
-    return {"ok": ok, "encode_ms": round(times[0] * 1e3, 2), "encode_reduce_ms": round(times[1] * 1e3, 2),
-            "retrieve_ms": round((t4 - t3) * 1e3, 2), "index_ct": n_idx, "payload_ct": n_pay,
-            "digest_bytes": int(d_dig.numel() * 8), "collective": "reduce(sum) over RCCL" if dist else "none",
-            "pertinent_recovered": len(indices)}
+def rooflines(role, dom, launches, per_launch_msgs, launch_ms_total, value, world):
+    """Dominant-kernel rooflines from HIP-event launch times and committed counter summaries.
+    The binding resource is FP64 VALU issue: `roofline` prices the kernel's FP64
+    FLOPs per launch (counted per message by rocprofv3 SQ_INSTS_VALU_*_F64, FMA = 2) against the
+    78.6 TFLOP/s FP64 peak. `hbm` gives the key-streaming figure of SURVEY.md §8(d) (every key
+    byte counted once per message: the north-star "fraction of HBM roofline") next to the HBM
+    bytes the counters measured (FETCH_SIZE x 2 per the gfx950 correction + WRITE_SIZE)."""
+    avg_launch_s = launch_ms_total / 1e3 / launches
+    pmc, comp = load_profile("pmc_latest.json"), load_profile("compute_latest.json")
+    traffic = None
+    if pmc and dom in pmc.get("kernels", {}) and pmc.get("messages_per_launch"):
+        traffic = pmc["kernels"][dom]["hbm_bytes_per_launch"] * per_launch_msgs / pmc["messages_per_launch"]
+    key_stream = KERNEL_BYTES[role] * per_launch_msgs / avg_launch_s / 1e9
+    hbm = {"key_stream_equiv_GBps": round(key_stream, 1), "key_stream_frac": round(key_stream / HBM_PEAK_GBS, 4),
+           "measured_GBps": None if traffic is None else round(traffic / avg_launch_s / 1e9, 1),
+           "measured_frac": None if traffic is None else round(traffic / avg_launch_s / 1e9 / HBM_PEAK_GBS, 4),
+           "whole_detect_key_stream_frac": round(value / world * DETECT_BYTES / 1e9 / HBM_PEAK_GBS, 4),
+           "peak": HBM_PEAK_GBS, "unit": "GB/s"}
+    roof = None
+    if comp and dom in comp.get("kernels", {}):
+        k = comp["kernels"][dom]
+        tflops = k["fp64_flop_per_msg"] * per_launch_msgs / avg_launch_s / 1e12
+        roof = {"bound": "fp64-valu", "kernel": dom, "achieved": round(tflops, 2),
+                "peak": round(FP64_PEAK_TFLOPS, 2), "unit": "TFLOP/s", "frac": round(tflops / FP64_PEAK_TFLOPS, 4),
+                "traffic": None if traffic is None else round(traffic),
+                "avg_launch_ms": round(avg_launch_s * 1e3, 2), "messages_per_launch": per_launch_msgs,
+                "fp64_lane_instr_frac": round(k["fp64_lane_instr_per_msg"] * per_launch_msgs / avg_launch_s
+                                              / (FP64_PEAK_TFLOPS / 2 * 1e12), 4),
+                "counts_from": comp.get("source")}
+    return roof, hbm
 
 
 def main():
@@ -170,19 +207,22 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
     if world > 1 or args.force_dist:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist.init_process_group("nccl", device_id=dev)
     else:
         dist = None
-        torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    D = args.messages
+    strong = args.total_messages is not None
+    if strong:
+        first, D, total = omr_dist.plan(rank, world, total=args.total_messages)
+    else:
+        first, D, total = omr_dist.plan(rank, world, per_gpu=args.messages or 65536)
 
     # keys + synthetic clues (identical on every rank: seeded, counter-based streams), generated on
-    # the GPU (bit-identical to the host generators, tests/test_gpu_parity.py)
+    # the GPU (bit-identical to the host generators and the oracle's)
     t0 = time.perf_counter()
     pack_a, pack_b = A.SecretKeyPack(42), A.SecretKeyPack(4242)
     cur = torch.cuda.current_stream(dev).cuda_stream
@@ -191,13 +231,11 @@ def main():
                                (A.BSK2_SHAPE, torch.int64), (A.TK_SHAPE, torch.int64))]
     pack_a.generate_detection_key_device(7, *[b.data_ptr() for b in kbufs], stream=cur)
     det = A.Detector.from_device_key(*[b.data_ptr() for b in kbufs], device=local)
-    first = rank * D
-    total = D * world
+    det.set_batch(args.batch)
     rng = np.random.default_rng(2025)
     pert = np.sort(rng.choice(total, min(args.pertinent, total), replace=False))
     mask = np.zeros(D, dtype=bool)
-    mine = pert[(pert >= first) & (pert < first + D)] - first
-    mask[mine] = True
+    mask[pert[(pert >= first) & (pert < first + D)] - first] = True
     d_ca = torch.empty((D, A.N0), dtype=torch.int16, device=dev)
     d_cb = torch.empty((D, A.CLUE_COUNT), dtype=torch.int16, device=dev)
     d_na, d_nb = torch.empty_like(d_ca), torch.empty_like(d_cb)
@@ -210,14 +248,12 @@ def main():
     torch.cuda.synchronize(dev)
     setup_s = time.perf_counter() - t0
 
-    d_out = torch.empty((D, 2, 2048), dtype=torch.int64, device=dev)
     stream = torch.cuda.current_stream(dev)
-
-    def step():
-        det.detect_batch_device(d_ca.data_ptr(), d_cb.data_ptr(), D, d_out.data_ptr(), stream.cuda_stream)
+    backend = omr_dist.GpuBackend(det, dev, stream)
+    d_out = torch.empty((D, 2, 2048), dtype=torch.int64, device=dev)
 
     for _ in range(args.warmup):
-        step()
+        backend.detect(d_ca, d_cb, out=d_out)
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
@@ -228,7 +264,7 @@ def main():
     t = time.perf_counter()
     start.record(stream)
     for i in range(args.steps):
-        step()
+        backend.detect(d_ca, d_cb, out=d_out)
         info = det.last_timing()  # per-stage HIP events recorded on `stream` (waits for them)
         for k in stage:
             stage[k] += info[k]
@@ -249,10 +285,28 @@ def main():
     # correctness spot check on this rank's data: the client decrypts (library Retriever, CPU)
     # and every pertinency ciphertext must decode to [1, 0, ..., 0] or all zeros (omd.rs:48-58)
     host = d_out[: min(D, 256)].cpu().numpy().view(np.uint64)
-    dec = A.Retriever(A.RetrievalParams(max(1, D), 1), pack_a).decrypt_decode(host)
+    dec = A.Retriever(A.RetrievalParams(max(1, total), 1), pack_a).decrypt_decode(host)
     ok = bool(np.array_equal(dec[:, 0] == 1, mask[: host.shape[0]]) and not dec[:, 1:].any())
 
-    e2e = None if args.no_e2e else end_to_end(det, pack_a, d_out, D, first, total, pert, dist, dev, stream, rank)
+    e2e = None
+    if not args.no_e2e:
+        rp = A.RetrievalParams(total, len(pert))
+        weights = A.payload_weights(WEIGHT_SEED, rp)
+        digest, et = omr_dist.encode_and_reduce(backend, d_out, synthetic_payloads(first, D), first, total, rp,
+                                                INDEX_SEED, weights, dist)
+        if rank == 0:
+            t3 = time.perf_counter()
+            indices, pays = A.Retriever(rp, pack_a).decode_digest(digest.indices, digest.payloads, WEIGHT_SEED)
+            t4 = time.perf_counter()
+            good = indices == [int(v) for v in pert]
+            if good:
+                want = np.concatenate([synthetic_payloads(int(i), 1) for i in indices]) if indices else np.zeros((0, 612))
+                good = bool(np.array_equal(pays, want))
+            e2e = {"ok": good, "encode_ms": round(et["encode_s"] * 1e3, 2),
+                   "encode_reduce_ms": round(et["encode_reduce_s"] * 1e3, 2), "retrieve_ms": round((t4 - t3) * 1e3, 2),
+                   "index_ct": rp.max_encode_indices_cipher_count, "payload_ct": rp.cmb_cipher_count,
+                   "digest_bytes": int((rp.max_encode_indices_cipher_count + rp.cmb_cipher_count) * 2 * 2048 * 8),
+                   "collective": "reduce(sum) over RCCL" if dist else "none", "pertinent_recovered": len(indices)}
 
     latency_ms = None
     if not args.no_latency:
@@ -271,32 +325,13 @@ def main():
             dist.destroy_process_group()
         return
 
-    msgs = args.steps * D * world
+    msgs = args.steps * total
     value = msgs / elapsed
-    # roofline of the dominant kernel: algorithmic bytes per launch / average launch duration,
-    # both from HIP events the library records on `stream` around each launch
     names = A.detect_kernels()
     kms = {"br1": stage["first_level_ms"], "ks": stage["key_switch_ms"], "br2": stage["second_level_ms"]}
     role = max(kms, key=kms.get)
-    dom = names[role]
-    chunks = -(-D // 16384)
-    launches = args.steps * chunks
-    avg_launch_s = kms[role] / 1e3 / launches
-    per_launch_msgs = D / chunks
-    achieved = KERNEL_BYTES[role] * per_launch_msgs / avg_launch_s / 1e9
-    pmc = load_profile("pmc_latest.json")
-    traffic = None
-    if pmc and dom in pmc.get("kernels", {}) and pmc.get("messages_per_launch"):
-        traffic = pmc["kernels"][dom]["hbm_bytes_per_launch"] * per_launch_msgs / pmc["messages_per_launch"]
-    comp = load_profile("compute_latest.json")
-    compute = None
-    if comp and dom in comp.get("kernels", {}):
-        lane_instr = comp["kernels"][dom]["fp64_lane_instr_per_msg"] * per_launch_msgs / avg_launch_s / 1e12
-        flops = comp["kernels"][dom]["fp64_flop_per_msg"] * per_launch_msgs / avg_launch_s / 1e12
-        compute = {"bound": "fp64-valu", "kernel": dom, "achieved": round(lane_instr, 2),
-                   "peak": round(FP64_PEAK_T_LANE_INSTR, 2), "unit": "T FP64 lane-instr/s",
-                   "frac": round(lane_instr / FP64_PEAK_T_LANE_INSTR, 4), "tflops": round(flops, 2),
-                   "counts_from": comp.get("source")}
+    chunks = -(-D // args.batch)
+    roof, hbm = rooflines(role, names[role], args.steps * chunks, D / chunks, kms[role], value, world)
     line = {
         "metric": "detect-phase messages/sec + per-message latency, D=65536 at 1/2/4/8 MI355X",
         "value": round(value, 2),
@@ -306,33 +341,30 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 2),
         "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": round(value / PUBLISHED_CPU_MSG_S, 1),
-        "vs_baseline_ref": "published 1-thread AVX-512 CPU detect, 234.07 ms/msg (README.md:122)",
+        "scaling": "strong" if strong else "weak",
+        "vs_baseline": round(value / (1e3 / PUBLISHED_CPU_MS_PER_MSG), 1),
+        "vs_baseline_ref": "published reference detect(), 1 thread AVX-512 CPU, 234.07 ms/msg at D=65,536 "
+                           "(README.md:122, BASELINE.md §1)",
         "dtype": "f64",
-        "data": "synthetic (seeded keys and clues; 50 pertinent over the whole job)",
-        "config": {"workload": workload_name(D, world),
-                   "messages_per_gpu": D, "messages_total": D * world,
-                   "pertinent": int(len(pert)), "batch": 16384, "parallelism": f"dp{world}"},
+        "data": "synthetic (seeded keys and clues generated on the GPU; 50 pertinent over the whole job)",
+        "config": {"workload": workload_name(D, total, world, strong),
+                   "messages_per_gpu": D, "messages_total": total,
+                   "pertinent": int(len(pert)), "batch": args.batch, "parallelism": f"dp{world}"},
         "latency_ms_per_message": latency_ms,
         "stage_ms_per_step": {k: round(v / args.steps, 2) for k, v in stage.items()},
         "detect_bytes_per_message": DETECT_BYTES,
-        "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": None if traffic is None else round(traffic),
-                     "whole_detect_achieved": round(value / world * DETECT_BYTES / 1e9, 1),
-                     "whole_detect_frac": round(value / world * DETECT_BYTES / 1e9 / HBM_PEAK_GBS, 4)},
-        "compute": compute,
+        "roofline": roof,
+        "hbm": hbm,
         "correct": ok,
         "e2e": e2e,
         "setup_s": round(setup_s, 1),
     }
     if not args.no_cpu_baseline and world == 1:
-        n = args.cpu_baseline_msgs
+        n = max(args.cpu_single_msgs, args.cpu_msgs_per_thread * cpu_threads())
         dk = A.DetectionKey(*[b.cpu().numpy().view(np.uint32 if b.dtype == torch.int32 else np.uint64).reshape(shape)
                               for b, shape in zip(kbufs, (A.BSK1_SHAPE, A.KSK_SHAPE, A.BSK2_SHAPE, A.TK_SHAPE))])
-        line["cpu_baseline"] = cpu_baseline(dk, d_ca[:n].cpu().numpy().view(np.uint16),
-                                            d_cb[:n].cpu().numpy().view(np.uint16), n)
+        ca, cb = pack_a.gen_clues(1000, 0, n)  # the same clue stream as the GPU workload
+        line["cpu_baseline"] = cpu_baseline(dk, ca, cb, args.cpu_single_msgs, args.cpu_msgs_per_thread)
     print(json.dumps(line), file=json_out, flush=True)
     if dist:
         dist.destroy_process_group()

@@ -151,18 +151,21 @@ typedef struct {
 
 omr_status omr_ctx_create(const omr_detection_key_view *key, int device, omr_ctx **out);
 void omr_ctx_destroy(omr_ctx *ctx);
-/* Messages per internal batch (memory/latency knob); 0 = default. */
 /* Kernel names of this build's detect pipeline: "br1=<name> ks=<name> br2=<name>". */
 const char *omr_detect_kernels(void);
+/* Messages per internal detect chunk (memory/latency knob: 36 KiB of scratch per message);
+ * 0 = the default 16,384. */
 omr_status omr_ctx_set_batch(omr_ctx *ctx, size_t batch);
 
 /* Detector::detect (detector.rs:135-166), batched like `par_iter().map(detect)` in
- * examples/omr.rs:219-223. Host buffers: clue_a u16 [D][512], clue_b u16 [D][7],
+ * examples/omr.rs:160-164. Host buffers: clue_a u16 [D][512], clue_b u16 [D][7],
  * out u64 [D][2][2048] (NTT domain). */
 omr_status omr_detect_batch(omr_ctx *ctx, const uint16_t *clue_a, const uint16_t *clue_b,
                             size_t D, uint64_t *out);
 /* Same on device buffers, enqueued on `hip_stream` (NULL = the context's stream);
- * returns once enqueued. */
+ * returns once enqueued. Calls on one context may use different streams: they share the
+ * context's scratch, so a call's kernels wait (hipStreamWaitEvent) for those of the previous
+ * call on another stream; the caller orders its own buffers. */
 omr_status omr_detect_batch_device(omr_ctx *ctx, const uint16_t *d_clue_a,
                                    const uint16_t *d_clue_b, size_t D, uint64_t *d_out,
                                    void *hip_stream);

@@ -1,7 +1,8 @@
 """world_size-2 gloo test of the multi-GPU orchestration (tfhe-omr_amd/omr_dist.py) on CPU.
-The compute backend is the CPU oracle (test-only); the sharding, global offsets and the digest
-reduce are the production code. The 2-rank digest must equal the 1-rank digest bit-for-bit
-and decode to the pertinent indices and payloads (omr_time_analyze.rs:215-235)."""
+The compute backend is the CPU oracle (test-only); the shard plan, global offsets, encode +
+digest reduce (omr_dist.encode_and_reduce, the function bench.py calls with the GPU backend)
+are the production code. The 2-rank digest must equal the 1-rank digest bit-for-bit and decode
+to the pertinent indices and payloads (omr_time_analyze.rs:215-235)."""
 import os
 import socket
 
@@ -22,18 +23,22 @@ WSEED = bytes(range(5, 37))
 
 
 class OracleBackend:
+    """omr_dist backend interface on the CPU oracle (host numpy buffers, torch CPU digest)."""
+
     def __init__(self, dk):
         self.det = O.OracleDetector(dk.bsk1, dk.ksk, dk.bsk2, dk.trace_key)
 
-    def detect_batch(self, ca, cb):
+    def synchronize(self):
+        pass
+
+    def detect(self, ca, cb):
         return self.det.detect_batch(ca, cb, nthreads=2)
 
-    def encode_pertinent_indices(self, rp, pv, seed, ct, off):
-        return O.encode_indices(pv, off, rp.all_payloads_count, seed, ct)
-
-    def encode_pertinent_payloads(self, pv, payloads, w, rp, off):
-        return O.encode_payloads(pv, payloads, off, rp.all_payloads_count, w, rp.cmb_cipher_count,
-                                 rp.cmb_count_per_cipher)
+    def encode(self, pv, payloads, first, total, rp, seed, w):
+        import torch
+        idx = [O.encode_indices(pv, first, total, seed, ct) for ct in range(rp.max_encode_indices_cipher_count)]
+        pay = O.encode_payloads(pv, payloads, first, total, w, rp.cmb_cipher_count, rp.cmb_count_per_cipher)
+        return torch.from_numpy(np.concatenate([np.stack(idx), pay]).astype(np.int64))
 
 
 def shard_inputs(first, count):
@@ -52,7 +57,8 @@ def _worker(rank, world, port, out_dir):
     _, _, dk = PL.keys()
     rp = A.RetrievalParams(TOTAL, int(MASK.sum()))
     w = A.payload_weights(WSEED, rp)
-    first, count = omr_dist.shard_range(rank, world, TOTAL)
+    first, count, total = omr_dist.plan(rank, world, total=TOTAL)
+    assert total == TOTAL
     ca, cb, pay = shard_inputs(first, count)
     _, dg = omr_dist.run_omr_shard(OracleBackend(dk), ca, cb, pay, first, TOTAL, rp, INDEX_SEED, w, dist=dist)
     if rank == 0:
@@ -67,6 +73,17 @@ def _free_port():
     p = s.getsockname()[1]
     s.close()
     return p
+
+
+def test_plan_weak_and_strong():
+    assert omr_dist.plan(3, 8, per_gpu=65536) == (3 * 65536, 65536, 524288)
+    spans = [omr_dist.plan(r, 4, total=524288) for r in range(4)]
+    assert spans == [(r * 131072, 131072, 524288) for r in range(4)]
+    assert [omr_dist.plan(r, 3, total=10)[:2] for r in range(3)] == [(0, 4), (4, 3), (7, 3)]
+    with pytest.raises(ValueError):
+        omr_dist.plan(0, 1)
+    with pytest.raises(ValueError):
+        omr_dist.plan(0, 1, per_gpu=1, total=1)
 
 
 def test_shard_range_partitions():

@@ -2,10 +2,11 @@
 // include/omr_gpu.h for the detect / encode path.
 //
 // Detector::new (detector.rs:85-110) -> omr_ctx_create: uploads the coefficient-domain keys,
-// converts them on the GPU to centred FP64 NTT-domain rows (N^-1 folded into the external-
-// product keys) and builds the LUTs (:457-503). Detector::detect (:135-166) for a batch of
-// messages -> four launches per chunk: br1_kernel (7 blind rotations per message), sum7_kernel,
-// ks_kernel, br2_trace_kernel.
+// converts them on the GPU (BSK1 to the FFT domain x 1/512, BSK2 and the trace key to centred
+// FP64 NTT-domain rows with N^-1 folded into the external-product keys, the KSK to int8 limbs)
+// and builds the LUTs (:457-503). Detector::detect (:135-166) for a batch of messages -> four
+// launches per chunk: br1f_kernel (7 blind rotations per message), sum7_kernel, ks_mfma_kernel,
+// br2_trace_kernel.
 #include <algorithm>
 #include <cstring>
 #include <mutex>
@@ -101,85 +102,88 @@ std::vector<double2> fft_twiddles(int T, int E, int L) {
 struct omr_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
-  Key1T *bsk1 = nullptr;    // level-1 NTT-domain keys (OMR_FFT1 == 0)
-  double2 *bsk1f = nullptr; // level-1 FFT-domain keys (OMR_FFT1)
-  double2 *fft1 = nullptr, *fft2 = nullptr, *fft2w = nullptr;
-  double2 *bsk2f = nullptr; // level-2 FFT-domain key limbs (OMR_FFT2)
+  double2 *bsk1f = nullptr;  // level-1 FFT-domain keys [512][8][2][512] complex, x 1/512
+  double2 *fft1 = nullptr;   // level-1 FFT twiddles
   double *bsk2 = nullptr, *tk = nullptr;
-  uint32_t *ksk = nullptr;
-  uint32_t *kskb = nullptr;  // OMR_KS_MFMA: int8 limbs of the KSK, [1024][4][672][32]
+  uint32_t *kskb = nullptr;  // int8 limbs of the KSK, [1024][4][672][32] (matrix-core key switch)
   double *tables = nullptr;  // tw1 itw1 tw2 itw2 lut1 lut2
   uint16_t *trace_tabs = nullptr;
   DeviceTables tb{};
   size_t batch = OMR_DEFAULT_BATCH, batch_cap = 0;
   uint32_t *ext = nullptr, *lwe1t = nullptr, *lwe_int = nullptr;
-  // OMR_OVERLAP: second stream for level 2 and a second LWE buffer (chunk c's level 2 runs
-  // while chunk c + 1's level 1 does)
-  hipStream_t stream2 = nullptr;
-  uint32_t *lwe_int2 = nullptr;
-  std::vector<hipEvent_t> ov_events;
   // host-API staging
   uint16_t *s_clue_a = nullptr, *s_clue_b = nullptr;
   uint64_t *s_out = nullptr;
   size_t staged = 0;
   // encode workspace
   uint64_t *partial = nullptr;
+  size_t partial_cap = 0;
+  // The scratch above is shared by every call on the context, while device-buffer calls only
+  // enqueue on the caller's stream: the last stream that used it records scratch_free, and a call
+  // on another stream waits for that event before its first kernel.
+  hipEvent_t scratch_free = nullptr;
+  hipStream_t scratch_stream = nullptr;
   // omr_detect_batch stages the host input in pieces of `batch` messages: their stage times are
   // summed here so omr_last_timing covers the whole call (device-buffer calls read the events)
   omr_detect_timing host_timing{};
   bool host_timing_valid = false;
-  size_t partial_cap = 0;
   // timing
   bool timing = false;
-  std::vector<hipEvent_t> events;  // 5 per chunk
-  size_t timed_messages = 0;
+  std::vector<hipEvent_t> events;  // 4 per chunk
+  size_t timed_messages = 0, timed_chunks = 0;
   std::mutex mu;
 };
 
-#if OMR_FFT1
 #define OMR_BR1_NAME "br1f_kernel"
-#else
-#define OMR_BR1_NAME "br1_kernel"
-#endif
-#if OMR_KS_MFMA
 #define OMR_KS_NAME "ks_mfma_kernel"
-#else
-#define OMR_KS_NAME "ks_kernel"
-#endif
-#if OMR_BR2_SLICED
-#define OMR_BR2_NAME "br2s_trace_kernel"
-#elif OMR_FFT2
-#define OMR_BR2_NAME "br2f_trace_kernel"
-#else
 #define OMR_BR2_NAME "br2_trace_kernel"
-#endif
 
 namespace {
 
+// Frees a device allocation made by this library (a failure here leaves nothing to recover).
+template <typename T>
+void dev_free(T *&p) {
+  if (p) (void)hipFree((void *)p);
+  p = nullptr;
+}
+
+// Scratch reuse across streams (see omr_ctx::scratch_free). Callers hold c->mu.
+omr_status scratch_acquire(omr_ctx *c, hipStream_t st) {
+  if (c->scratch_stream && c->scratch_stream != st) HIP_TRY(hipStreamWaitEvent(st, c->scratch_free, 0));
+  return OMR_OK;
+}
+omr_status scratch_release(omr_ctx *c, hipStream_t st) {
+  HIP_TRY(hipEventRecord(c->scratch_free, st));
+  c->scratch_stream = st;
+  return OMR_OK;
+}
+// Reallocating scratch: every stream that used it must be done first.
+omr_status scratch_idle(omr_ctx *c) {
+  if (c->scratch_stream) HIP_TRY(hipEventSynchronize(c->scratch_free));
+  return OMR_OK;
+}
+
 omr_status ensure_batch(omr_ctx *c, size_t B) {
   if (B <= c->batch_cap) return OMR_OK;
-  hipFree(c->ext);
-  hipFree(c->lwe1t);
-  hipFree(c->lwe_int);
-  c->ext = nullptr;
-  c->lwe1t = nullptr;
-  c->lwe_int = nullptr;
+  omr_status s;
+  if ((s = scratch_idle(c)) != OMR_OK) return s;
+  dev_free(c->ext);
+  dev_free(c->lwe1t);
+  dev_free(c->lwe_int);
+  c->batch_cap = 0;
   HIP_TRY(hipMalloc(&c->ext, B * CLUES * (N1 + 1) * sizeof(uint32_t)));
   HIP_TRY(hipMalloc(&c->lwe1t, B * (N1 + 1) * sizeof(uint32_t)));
   HIP_TRY(hipMalloc(&c->lwe_int, B * (NI + 1) * sizeof(uint32_t)));
-  if (OMR_OVERLAP) {
-    hipFree(c->lwe_int2);
-    c->lwe_int2 = nullptr;
-    HIP_TRY(hipMalloc(&c->lwe_int2, B * (NI + 1) * sizeof(uint32_t)));
-  }
   c->batch_cap = B;
   return OMR_OK;
 }
 
 omr_status ensure_partial(omr_ctx *c, size_t elems) {
   if (elems <= c->partial_cap) return OMR_OK;
-  hipFree(c->partial);
-  c->partial = nullptr;
+  omr_status s;
+  if ((s = scratch_idle(c)) != OMR_OK) return s;
+  dev_free(c->partial);
+  c->partial_cap = 0;
   HIP_TRY(hipMalloc(&c->partial, elems * sizeof(uint64_t)));
   c->partial_cap = elems;
   return OMR_OK;
@@ -200,7 +204,7 @@ omr_status convert_keys(const IN *host, size_t npoly, OUT *dev, double scale, co
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(st));
   }
-  hipFree(tmp);
+  dev_free(tmp);
   return OMR_OK;
 }
 
@@ -216,82 +220,32 @@ omr_status convert_keys_fft1(const uint32_t *host, size_t npoly, double2 *dev, c
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(st));
   }
-  hipFree(tmp);
+  dev_free(tmp);
   return OMR_OK;
 }
 
 // LWE key switch + modulus switch of B messages (lwe1t [1025][B] -> out [B][671]).
 omr_status launch_ks(omr_ctx *c, int B, uint32_t *out, hipStream_t st) {
-  if (OMR_KS_MFMA)
-    ks_mfma_kernel<<<dim3((B + 63) / 64, KSM_COLS / 32), 64, 0, st>>>(c->lwe1t, c->kskb, out, B);
-  else
-    ks_kernel<KS_CT><<<dim3((B + 63) / 64, (NI + 1 + KS_CT - 1) / KS_CT), 64, 0, st>>>(c->lwe1t, c->ksk, out, B);
+  ks_mfma_kernel<<<dim3((B + 63) / 64, KSM_COLS / 32), 64, 0, st>>>(c->lwe1t, c->kskb, out, B);
   HIP_TRY(hipGetLastError());
   return OMR_OK;
 }
 
-// Level-1 blind rotations: n workgroups (mode 0: clue wg%7 of message wg/7 -> extracted LWE;
-// mode 1: explicit LWEs -> full RLWE).
+// Level-1 blind rotations of n (message, clue) pairs (mode 0: clue g % 7 of message g / 7 ->
+// extracted LWE; mode 1: explicit LWEs -> full RLWE), BR1F_WPG rotations per workgroup.
 omr_status launch_br1(omr_ctx *c, size_t n, const uint16_t *ca, const uint16_t *cb,
                       const uint16_t *la, const uint16_t *lb, uint32_t *ext, uint64_t *rlwe, int mode,
                       hipStream_t st) {
-#if OMR_FFT1
-  constexpr size_t per_wg = (size_t)BR1F_RW * BR1F_WPG;
-  br1f_kernel<BR1F_RW><<<(unsigned)((n + per_wg - 1) / per_wg), 64 * BR1F_WPG, 0, st>>>(
+  br1f_kernel<<<(unsigned)((n + BR1F_WPG - 1) / BR1F_WPG), 64 * BR1F_WPG, 0, st>>>(
       ca, cb, la, lb, c->bsk1f, c->tb, ext, rlwe, mode, n);
-#else
-  br1_kernel<<<(unsigned)n, BR1_T, 0, st>>>(ca, cb, la, lb, c->bsk1, c->tb, ext, rlwe, mode);
-#endif
   HIP_TRY(hipGetLastError());
   return OMR_OK;
 }
 
-omr_status convert_keys_fft2(const uint64_t *host, size_t npoly, double2 *dev, const double2 *tw,
-                             hipStream_t st) {
-  const size_t chunk = 4096;
-  uint64_t *tmp = nullptr;
-  HIP_TRY(hipMalloc(&tmp, chunk * N2 * sizeof(uint64_t)));
-  for (size_t p0 = 0; p0 < npoly; p0 += chunk) {
-    const size_t n = std::min(chunk, npoly - p0);
-    HIP_TRY(hipMemcpyAsync(tmp, host + p0 * N2, n * N2 * sizeof(uint64_t), hipMemcpyDefault, st));
-    key_to_fft2_kernel<<<n, 256, 0, st>>>(tmp, dev + p0 * 2 * Fft1024::N, n, tw);
-    HIP_TRY(hipGetLastError());
-    HIP_TRY(hipStreamSynchronize(st));
-  }
-  (void)hipFree(tmp);
-  return OMR_OK;
-}
-
-// Level-2 blind rotation (+ trace, mode 0) of n LWE(670, 4096) ciphertexts.
+// Level-2 blind rotation (+ trace, mode 0) of n LWE(670, 4096) ciphertexts, one workgroup each.
 omr_status launch_br2(omr_ctx *c, size_t n, const uint32_t *lwe_int, uint64_t *out, int mode,
                       hipStream_t st) {
-#if OMR_BR2_SLICED
-  br2s_trace_kernel<<<(unsigned)n, BR2_T, 0, st>>>(lwe_int, c->bsk2f, c->tk, c->tb, out, mode);
-#else
-#if OMR_FFT2
-  auto kern = br2f_trace_kernel;
-  const auto *keys = c->bsk2f;
-#else
-  auto kern = br2_trace_kernel;
-  const auto *keys = c->bsk2;
-#endif
-  size_t gen = n;
-  if (OMR_BR2_PERSIST) {
-    // Launch in generations of one resident grid each: the workgroups of a generation start
-    // together and do the same work, so they stay near the same CMUX step and share each key
-    // row through L2, instead of drifting over the whole key as replacement workgroups would.
-    int dev = 0, cus = 0, per_cu = 0;
-    HIP_TRY(hipGetDevice(&dev));
-    HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, BR2_T, 0));
-    gen = std::max<size_t>(1, (size_t)cus * (size_t)(per_cu > 0 ? per_cu : 1));
-  }
-  for (size_t off = 0; off < n; off += gen) {
-    const size_t m = std::min(gen, n - off);
-    kern<<<(unsigned)m, BR2_T, 0, st>>>(lwe_int + off * (NI + 1), keys, c->tk, c->tb,
-                                        out + off * 2 * N2, mode);
-  }
-#endif
+  br2_trace_kernel<<<(unsigned)n, BR2_T, 0, st>>>(lwe_int, c->bsk2, c->tk, c->tb, out, mode);
   HIP_TRY(hipGetLastError());
   return OMR_OK;
 }
@@ -321,8 +275,9 @@ extern "C" omr_status omr_ctx_create(const omr_detection_key_view *key, int devi
     omr_ctx_destroy(c);
     return st;
   };
-  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
-    return fail(set_error(OMR_ERR_DEVICE, "hipStreamCreate failed"));
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&c->scratch_free, hipEventDisableTiming) != hipSuccess)
+    return fail(set_error(OMR_ERR_DEVICE, "hipStreamCreate / hipEventCreate failed"));
   // tables
   std::vector<double> tw1, itw1, tw2, itw2;
   twiddles(Q1, N1, 7, tw1, itw1);
@@ -351,8 +306,9 @@ extern "C" omr_status omr_ctx_create(const omr_detection_key_view *key, int devi
   if (hipMalloc(&c->tables, tabs.size() * sizeof(double)) != hipSuccess ||
       hipMalloc(&c->trace_tabs, ttab.size() * sizeof(uint16_t)) != hipSuccess)
     return fail(set_error(OMR_ERR_OUT_OF_MEMORY, "omr_ctx_create: tables"));
-  hipMemcpy(c->tables, tabs.data(), tabs.size() * sizeof(double), hipMemcpyHostToDevice);
-  hipMemcpy(c->trace_tabs, ttab.data(), ttab.size() * sizeof(uint16_t), hipMemcpyHostToDevice);
+  if (hipMemcpy(c->tables, tabs.data(), tabs.size() * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(c->trace_tabs, ttab.data(), ttab.size() * sizeof(uint16_t), hipMemcpyHostToDevice) != hipSuccess)
+    return fail(set_error(OMR_ERR_DEVICE, "omr_ctx_create: table upload"));
   c->tb.tw1 = c->tables;
   c->tb.itw1 = c->tables + N1;
   c->tb.tw2 = c->tables + 2 * N1;
@@ -364,53 +320,35 @@ extern "C" omr_status omr_ctx_create(const omr_detection_key_view *key, int devi
   const auto ftw = fft_twiddles(Fft512::T, Fft512::E, Fft512::L);
   if (hipMalloc(&c->fft1, ftw.size() * sizeof(double2)) != hipSuccess)
     return fail(set_error(OMR_ERR_OUT_OF_MEMORY, "omr_ctx_create: tables"));
-  hipMemcpy(c->fft1, ftw.data(), ftw.size() * sizeof(double2), hipMemcpyHostToDevice);
+  if (hipMemcpy(c->fft1, ftw.data(), ftw.size() * sizeof(double2), hipMemcpyHostToDevice) != hipSuccess)
+    return fail(set_error(OMR_ERR_DEVICE, "omr_ctx_create: table upload"));
   c->tb.fft1 = c->fft1;
-  const auto ftw2 = fft_twiddles(Fft1024::T, Fft1024::E, Fft1024::L);
-  if (hipMalloc(&c->fft2, ftw2.size() * sizeof(double2)) != hipSuccess)
-    return fail(set_error(OMR_ERR_OUT_OF_MEMORY, "omr_ctx_create: tables"));
-  hipMemcpy(c->fft2, ftw2.data(), ftw2.size() * sizeof(double2), hipMemcpyHostToDevice);
-  c->tb.fft2 = c->fft2;
-  const auto ftw2w = fft_twiddles(Fft1024W::T, Fft1024W::E, Fft1024W::L);
-  if (hipMalloc(&c->fft2w, ftw2w.size() * sizeof(double2)) != hipSuccess)
-    return fail(set_error(OMR_ERR_OUT_OF_MEMORY, "omr_ctx_create: tables"));
-  hipMemcpy(c->fft2w, ftw2w.data(), ftw2w.size() * sizeof(double2), hipMemcpyHostToDevice);
-  c->tb.fft2w = c->fft2w;
   // keys
-  const bool fft1 = OMR_FFT1 != 0, fft2 = OMR_FFT2 != 0 || OMR_BR2_SLICED != 0;
-  if ((fft1 ? hipMalloc(&c->bsk1f, BSK1_ELEMS / 2 * sizeof(double2))
-            : hipMalloc(&c->bsk1, BSK1_ELEMS * sizeof(Key1T))) != hipSuccess ||
-      (fft2 ? hipMalloc(&c->bsk2f, BSK2_ELEMS * sizeof(double2))
-            : hipMalloc(&c->bsk2, BSK2_ELEMS * sizeof(double))) != hipSuccess ||
+  if (hipMalloc(&c->bsk1f, BSK1_ELEMS / 2 * sizeof(double2)) != hipSuccess ||
+      hipMalloc(&c->bsk2, BSK2_ELEMS * sizeof(double)) != hipSuccess ||
       hipMalloc(&c->tk, TK_ELEMS * sizeof(double)) != hipSuccess ||
-      hipMalloc(&c->ksk, (KSK_ELEMS + 64) * sizeof(uint32_t)) != hipSuccess)
+      hipMalloc(&c->kskb, KSKB_WORDS * sizeof(uint32_t)) != hipSuccess)
     return fail(set_error(OMR_ERR_OUT_OF_MEMORY, "omr_ctx_create: key buffers"));
-  const double ninv1 = centred(h_powmod(N1, Q1 - 2, Q1), Q1);
   const double ninv2 = centred(h_powmod(N2, Q2 - 2, Q2), Q2);
   omr_status st;
-  if ((st = fft1 ? convert_keys_fft1(key->bsk1, BSK1_ELEMS / N1, c->bsk1f, c->fft1, c->stream)
-                 : convert_keys<1, uint32_t, Key1T>(key->bsk1, BSK1_ELEMS / N1, c->bsk1, ninv1,
-                                                    c->tb.tw1, c->stream)) != OMR_OK)
+  if ((st = convert_keys_fft1(key->bsk1, BSK1_ELEMS / N1, c->bsk1f, c->fft1, c->stream)) != OMR_OK)
     return fail(st);
-  if ((st = fft2 ? convert_keys_fft2(key->bsk2, BSK2_ELEMS / N2, c->bsk2f, c->fft2, c->stream)
-                 : convert_keys<2, uint64_t, double>(key->bsk2, BSK2_ELEMS / N2, c->bsk2, ninv2,
-                                                     c->tb.tw2, c->stream)) != OMR_OK)
+  if ((st = convert_keys<2, uint64_t, double>(key->bsk2, BSK2_ELEMS / N2, c->bsk2, ninv2, c->tb.tw2,
+                                              c->stream)) != OMR_OK)
     return fail(st);
   if ((st = convert_keys<2, uint64_t, double>(key->trace_key, TK_ELEMS / N2, c->tk, 1.0, c->tb.tw2,
-                                      c->stream)) != OMR_OK)
+                                              c->stream)) != OMR_OK)
     return fail(st);
   scale_even_rows_kernel<<<(TK_ELEMS / N2 + 1) / 2, 256, 0, c->stream>>>(c->tk, TK_ELEMS / N2, ninv2);
-  if (hipMemcpyAsync(c->ksk, key->ksk, KSK_ELEMS * sizeof(uint32_t), hipMemcpyDefault,
-                     c->stream) != hipSuccess ||
-      hipMemsetAsync(c->ksk + KSK_ELEMS, 0, 64 * sizeof(uint32_t), c->stream) != hipSuccess ||
-      hipStreamSynchronize(c->stream) != hipSuccess)
-    return fail(set_error(OMR_ERR_DEVICE, "omr_ctx_create: key upload"));
-  if (OMR_KS_MFMA) {  // int8 limbs of the KSK for the matrix-core key switch (88 MB)
-    if (hipMalloc(&c->kskb, KSKB_WORDS * sizeof(uint32_t)) != hipSuccess)
-      return fail(set_error(OMR_ERR_OUT_OF_MEMORY, "omr_ctx_create: KSK limbs"));
-    ksk_to_i8_kernel<<<(unsigned)((KSKB_WORDS + 255) / 256), 256, 0, c->stream>>>(c->ksk, c->kskb);
-    if (hipGetLastError() != hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess)
-      return fail(set_error(OMR_ERR_DEVICE, "omr_ctx_create: KSK limbs"));
+  {  // the KSK goes to the device once, as the int8 limbs of the matrix-core key switch (88 MB)
+    uint32_t *ksk = nullptr;
+    const bool ok = hipMalloc(&ksk, (KSK_ELEMS + 64) * sizeof(uint32_t)) == hipSuccess &&
+                    hipMemcpyAsync(ksk, key->ksk, KSK_ELEMS * sizeof(uint32_t), hipMemcpyDefault, c->stream) == hipSuccess &&
+                    hipMemsetAsync(ksk + KSK_ELEMS, 0, 64 * sizeof(uint32_t), c->stream) == hipSuccess;
+    if (ok) ksk_to_i8_kernel<<<(unsigned)((KSKB_WORDS + 255) / 256), 256, 0, c->stream>>>(ksk, c->kskb);
+    const bool done = ok && hipGetLastError() == hipSuccess && hipStreamSynchronize(c->stream) == hipSuccess;
+    dev_free(ksk);
+    if (!done) return fail(set_error(OMR_ERR_DEVICE, "omr_ctx_create: KSK upload"));
   }
   if ((st = ensure_batch(c, c->batch)) != OMR_OK) return fail(st);
   *out = c;
@@ -419,21 +357,26 @@ extern "C" omr_status omr_ctx_create(const omr_detection_key_view *key, int devi
 
 extern "C" void omr_ctx_destroy(omr_ctx *c) {
   if (!c) return;
-  hipSetDevice(c->device);
-  if (c->stream) hipStreamSynchronize(c->stream);
-  for (void *p : {(void *)c->bsk1, (void *)c->bsk1f, (void *)c->fft1, (void *)c->fft2, (void *)c->fft2w, (void *)c->bsk2f, (void *)c->bsk2, (void *)c->tk, (void *)c->ksk, (void *)c->kskb,
-                  (void *)c->tables, (void *)c->trace_tabs, (void *)c->ext, (void *)c->lwe1t,
-                  (void *)c->lwe_int, (void *)c->s_clue_a, (void *)c->s_clue_b, (void *)c->s_out,
-                  (void *)c->partial})
-    if (p) hipFree(p);
-  for (auto e : c->events) hipEventDestroy(e);
-  for (auto e : c->ov_events) hipEventDestroy(e);
-  if (c->stream2) {
-    hipStreamSynchronize(c->stream2);
-    hipStreamDestroy(c->stream2);
-  }
-  if (c->lwe_int2) hipFree(c->lwe_int2);
-  if (c->stream) hipStreamDestroy(c->stream);
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->scratch_stream) (void)hipEventSynchronize(c->scratch_free);
+  dev_free(c->bsk1f);
+  dev_free(c->fft1);
+  dev_free(c->bsk2);
+  dev_free(c->tk);
+  dev_free(c->kskb);
+  dev_free(c->tables);
+  dev_free(c->trace_tabs);
+  dev_free(c->ext);
+  dev_free(c->lwe1t);
+  dev_free(c->lwe_int);
+  dev_free(c->s_clue_a);
+  dev_free(c->s_clue_b);
+  dev_free(c->s_out);
+  dev_free(c->partial);
+  for (auto e : c->events) (void)hipEventDestroy(e);
+  if (c->scratch_free) (void)hipEventDestroy(c->scratch_free);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
 
@@ -446,7 +389,7 @@ extern "C" omr_status omr_ctx_set_batch(omr_ctx *c, size_t batch) {
   if (!c) return set_error(OMR_ERR_INVALID_ARGUMENT, "omr_ctx_set_batch: NULL ctx");
   std::lock_guard<std::mutex> lk(c->mu);
   c->batch = batch ? batch : OMR_DEFAULT_BATCH;
-  hipSetDevice(c->device);
+  HIP_TRY(hipSetDevice(c->device));
   return ensure_batch(c, c->batch);
 }
 
@@ -458,66 +401,28 @@ extern "C" omr_status omr_ctx_enable_timing(omr_ctx *c, int enable) {
 
 namespace {
 
-// OMR_OVERLAP (experiment): level 1 + key switch of chunk c + 1 on st while level 2 of chunk c
-// runs on stream2; LWE buffers alternate, each reused only after the level 2 that read it.
-// Stage events: [0] br1 start, [1] br1 end, [2] ks end (st), [4] br2 start, [3] br2 end (stream2).
-omr_status detect_device_overlap(omr_ctx *c, const uint16_t *ca, const uint16_t *cb, size_t D,
-                                 uint64_t *out, hipStream_t st, size_t nchunks) {
-  if (!c->stream2) HIP_TRY(hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));
-  while (c->ov_events.size() < 2 * nchunks + 1) {
-    hipEvent_t e;
-    HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    c->ov_events.push_back(e);
-  }
-  hipEvent_t *ks_done = &c->ov_events[0], *br2_done = &c->ov_events[nchunks],
-             start = c->ov_events[2 * nchunks];
-  HIP_TRY(hipEventRecord(start, st));
-  HIP_TRY(hipStreamWaitEvent(c->stream2, start, 0));  // level 2 starts after the caller's prior work
-  for (size_t ch = 0; ch < nchunks; ++ch) {
-    const size_t off = ch * c->batch;
-    const int B = (int)std::min(c->batch, D - off);
-    uint32_t *lwe = (ch & 1) ? c->lwe_int2 : c->lwe_int;
-    hipEvent_t *ev = c->timing ? &c->events[ch * 5] : nullptr;
-    omr_status s;
-    if (ev) HIP_TRY(hipEventRecord(ev[0], st));
-    if ((s = launch_br1(c, (size_t)B * CLUES, ca + off * N0, cb + off * CLUES, nullptr, nullptr,
-                        c->ext, nullptr, 0, st)) != OMR_OK)
-      return s;
-    if (ev) HIP_TRY(hipEventRecord(ev[1], st));
-    const size_t n7 = (size_t)B * (N1 + 1);
-    sum7_kernel<<<(unsigned)((n7 + 255) / 256), 256, 0, st>>>(c->ext, c->lwe1t, B);
-    if (ch >= 2) HIP_TRY(hipStreamWaitEvent(st, br2_done[ch - 2], 0));  // its LWE buffer is free
-    if ((s = launch_ks(c, B, lwe, st)) != OMR_OK) return s;
-    if (ev) HIP_TRY(hipEventRecord(ev[2], st));
-    HIP_TRY(hipEventRecord(ks_done[ch], st));
-    HIP_TRY(hipStreamWaitEvent(c->stream2, ks_done[ch], 0));
-    if (ev) HIP_TRY(hipEventRecord(ev[4], c->stream2));
-    if ((s = launch_br2(c, (size_t)B, lwe, out + off * 2 * N2, 0, c->stream2)) != OMR_OK) return s;
-    if (ev) HIP_TRY(hipEventRecord(ev[3], c->stream2));
-    HIP_TRY(hipEventRecord(br2_done[ch], c->stream2));
-  }
-  HIP_TRY(hipStreamWaitEvent(st, br2_done[nchunks - 1], 0));  // the caller's stream sees the output
-  return OMR_OK;
-}
-
+// Detect D messages of device buffers on st, in chunks of c->batch: per chunk br1f (7 rotations
+// per message) -> sum7 -> key switch -> br2 + trace. Stage events [0] br1 start, [1] br1 end,
+// [2] key switch end, [3] br2 end per chunk.
 omr_status detect_device(omr_ctx *c, const uint16_t *ca, const uint16_t *cb, size_t D,
                          uint64_t *out, hipStream_t st) {
   omr_status s;
   if ((s = ensure_batch(c, std::min(D, c->batch))) != OMR_OK) return s;
   const size_t nchunks = (D + c->batch - 1) / c->batch;
   if (c->timing) {
-    while (c->events.size() < nchunks * 5) {
+    while (c->events.size() < nchunks * 4) {
       hipEvent_t e;
       HIP_TRY(hipEventCreate(&e));
       c->events.push_back(e);
     }
     c->timed_messages = D;
+    c->timed_chunks = nchunks;
   }
-  if (OMR_OVERLAP) return detect_device_overlap(c, ca, cb, D, out, st, nchunks);
+  if ((s = scratch_acquire(c, st)) != OMR_OK) return s;
   for (size_t ch = 0; ch < nchunks; ++ch) {
     const size_t off = ch * c->batch;
     const int B = (int)std::min(c->batch, D - off);
-    hipEvent_t *ev = c->timing ? &c->events[ch * 5] : nullptr;
+    hipEvent_t *ev = c->timing ? &c->events[ch * 4] : nullptr;
     if (ev) HIP_TRY(hipEventRecord(ev[0], st));
     if ((s = launch_br1(c, (size_t)B * CLUES, ca + off * N0, cb + off * CLUES, nullptr, nullptr,
                         c->ext, nullptr, 0, st)) != OMR_OK)
@@ -530,17 +435,15 @@ omr_status detect_device(omr_ctx *c, const uint16_t *ca, const uint16_t *cb, siz
     if ((s = launch_br2(c, (size_t)B, c->lwe_int, out + off * 2 * N2, 0, st)) != OMR_OK) return s;
     if (ev) HIP_TRY(hipEventRecord(ev[3], st));
   }
-  return OMR_OK;
+  return scratch_release(c, st);
 }
 
 omr_status stage_buffers(omr_ctx *c, size_t B) {
   if (B <= c->staged) return OMR_OK;
-  hipFree(c->s_clue_a);
-  hipFree(c->s_clue_b);
-  hipFree(c->s_out);
-  c->s_clue_a = nullptr;
-  c->s_clue_b = nullptr;
-  c->s_out = nullptr;
+  dev_free(c->s_clue_a);
+  dev_free(c->s_clue_b);
+  dev_free(c->s_out);
+  c->staged = 0;
   HIP_TRY(hipMalloc(&c->s_clue_a, B * N0 * sizeof(uint16_t)));
   HIP_TRY(hipMalloc(&c->s_clue_b, B * CLUES * sizeof(uint16_t)));
   HIP_TRY(hipMalloc(&c->s_out, B * 2 * N2 * sizeof(uint64_t)));
@@ -606,14 +509,13 @@ namespace {
 omr_status collect_timing(omr_ctx *c, omr_detect_timing *t) {
   memset(t, 0, sizeof(*t));
   if (!c->timing || c->timed_messages == 0) return OMR_OK;
-  const size_t nchunks = (c->timed_messages + c->batch - 1) / c->batch;
-  for (size_t ch = 0; ch < nchunks; ++ch) {
-    hipEvent_t *ev = &c->events[ch * 5];
+  for (size_t ch = 0; ch < c->timed_chunks; ++ch) {  // the chunk count of the timed call
+    hipEvent_t *ev = &c->events[ch * 4];
     HIP_TRY(hipEventSynchronize(ev[3]));
     float a = 0, b = 0, d = 0;
     HIP_TRY(hipEventElapsedTime(&a, ev[0], ev[1]));
     HIP_TRY(hipEventElapsedTime(&b, ev[1], ev[2]));
-    HIP_TRY(hipEventElapsedTime(&d, OMR_OVERLAP ? ev[4] : ev[2], ev[3]));
+    HIP_TRY(hipEventElapsedTime(&d, ev[2], ev[3]));
     t->first_level_ms += a;
     t->key_switch_ms += b;
     t->second_level_ms += d;
@@ -636,11 +538,20 @@ extern "C" omr_status omr_last_timing(omr_ctx *c, omr_detect_timing *t) {
 // ------------------------------------------------------------------------------------------
 // Encode (detector.rs:223-453)
 // ------------------------------------------------------------------------------------------
+namespace {
+// Messages per encode workgroup: at least 32 (128 from D = 16,384), and at most 4,096 chunk
+// partials per ciphertext (scratch n_ct x chunks x 32 KiB: 3.7 GB for 28 ciphertexts at D = 2^20).
+int encode_per_wg(size_t D) {
+  const size_t base = D >= 16384 ? 128 : 32;
+  return (int)std::max(base, (D + 4095) / 4096);
+}
+}  // namespace
+
 extern "C" omr_status omr_encode_indices_device(omr_ctx *c, const uint64_t *pv, size_t D,
                                                 size_t offset, size_t all, uint64_t seed,
                                                 uint32_t first_ct, uint32_t n_ct, uint64_t *out,
                                                 void *stream) {
-  if (!c || !out || (D && !pv) || n_ct == 0 || offset + D > all)
+  if (!c || !out || (D && !pv) || n_ct == 0 || offset + D > all || D > (size_t)INT32_MAX)
     return set_error(OMR_ERR_INVALID_ARGUMENT, "omr_encode_indices_device: bad argument");
   std::lock_guard<std::mutex> lk(c->mu);
   HIP_TRY(hipSetDevice(c->device));
@@ -652,9 +563,10 @@ extern "C" omr_status omr_encode_indices_device(omr_ctx *c, const uint64_t *pv, 
     HIP_TRY(hipMemsetAsync(out, 0, (size_t)n_ct * 2 * N2 * sizeof(uint64_t), st));
     return OMR_OK;
   }
-  const int per_wg = D >= 16384 ? 128 : 32;
+  const int per_wg = encode_per_wg(D);
   const int chunks = (int)((D + per_wg - 1) / per_wg);
   if ((s = ensure_partial(c, (size_t)n_ct * chunks * 2 * N2)) != OMR_OK) return s;
+  if ((s = scratch_acquire(c, st)) != OMR_OK) return s;
   EncodeLayout ly{(int)rp.index_slots_per_bucket, (int)rp.slots_per_bucket,
                   (int)rp.slots_per_segment, (int)rp.segment_per_cipher};
   encode_indices_kernel<<<dim3(chunks, n_ct), ENC_T, 0, st>>>(pv, (int)D, offset, ly, seed, first_ct,
@@ -663,7 +575,7 @@ extern "C" omr_status omr_encode_indices_device(omr_ctx *c, const uint64_t *pv, 
   const size_t tot = (size_t)n_ct * 2 * N2;
   reduce_partials_kernel<<<(unsigned)((tot + 255) / 256), 256, 0, st>>>(c->partial, chunks, (int)n_ct, out);
   HIP_TRY(hipGetLastError());
-  return OMR_OK;
+  return scratch_release(c, st);
 }
 
 extern "C" omr_status omr_encode_payloads_device(omr_ctx *c, const uint64_t *pv,
@@ -671,7 +583,7 @@ extern "C" omr_status omr_encode_payloads_device(omr_ctx *c, const uint64_t *pv,
                                                  size_t all, const uint16_t *weights, uint32_t n_ct,
                                                  uint32_t per_ct, uint64_t *out, void *stream) {
   if (!c || !out || (D && (!pv || !payloads || !weights)) || n_ct == 0 || per_ct == 0 ||
-      per_ct * PAYLOAD_LEN > (uint32_t)N2 || offset + D > all)
+      per_ct * PAYLOAD_LEN > (uint32_t)N2 || offset + D > all || D > (size_t)INT32_MAX)
     return set_error(OMR_ERR_INVALID_ARGUMENT, "omr_encode_payloads_device: bad argument");
   std::lock_guard<std::mutex> lk(c->mu);
   HIP_TRY(hipSetDevice(c->device));
@@ -680,10 +592,11 @@ extern "C" omr_status omr_encode_payloads_device(omr_ctx *c, const uint64_t *pv,
     HIP_TRY(hipMemsetAsync(out, 0, (size_t)n_ct * 2 * N2 * sizeof(uint64_t), st));
     return OMR_OK;
   }
-  const int per_wg = D >= 16384 ? 128 : 32;
+  const int per_wg = encode_per_wg(D);
   const int chunks = (int)((D + per_wg - 1) / per_wg);
   omr_status s;
   if ((s = ensure_partial(c, (size_t)n_ct * chunks * 2 * N2)) != OMR_OK) return s;
+  if ((s = scratch_acquire(c, st)) != OMR_OK) return s;
   encode_payloads_kernel<<<dim3(chunks, n_ct), ENC_T, 0, st>>>(pv, payloads, (int)D, offset, all,
                                                                weights, (int)per_ct, per_wg,
                                                                c->tb.tw2, c->partial);
@@ -691,7 +604,7 @@ extern "C" omr_status omr_encode_payloads_device(omr_ctx *c, const uint64_t *pv,
   const size_t tot = (size_t)n_ct * 2 * N2;
   reduce_partials_kernel<<<(unsigned)((tot + 255) / 256), 256, 0, st>>>(c->partial, chunks, (int)n_ct, out);
   HIP_TRY(hipGetLastError());
-  return OMR_OK;
+  return scratch_release(c, st);
 }
 
 namespace {
@@ -699,7 +612,7 @@ template <typename T>
 struct DevBuf {
   T *p = nullptr;
   ~DevBuf() {
-    if (p) hipFree(p);
+    if (p) (void)hipFree(p);
   }
   hipError_t alloc(size_t n) { return hipMalloc(&p, n * sizeof(T)); }
 };
@@ -708,7 +621,7 @@ struct DevBuf {
 extern "C" omr_status omr_encode_indices(omr_ctx *c, const uint64_t *pv, size_t D, size_t offset,
                                          size_t all, uint64_t seed, uint32_t ct, uint64_t *out) {
   if (!c || !out || (D && !pv)) return set_error(OMR_ERR_INVALID_ARGUMENT, "omr_encode_indices");
-  hipSetDevice(c->device);
+  HIP_TRY(hipSetDevice(c->device));
   DevBuf<uint64_t> dpv, dout;
   HIP_TRY(dpv.alloc(std::max<size_t>(D, 1) * 2 * N2));
   HIP_TRY(dout.alloc(2 * N2));
@@ -726,7 +639,7 @@ extern "C" omr_status omr_encode_payloads(omr_ctx *c, const uint64_t *pv, const 
                                           uint64_t *out) {
   if (!c || !out || (D && (!pv || !payloads || !weights)))
     return set_error(OMR_ERR_INVALID_ARGUMENT, "omr_encode_payloads");
-  hipSetDevice(c->device);
+  HIP_TRY(hipSetDevice(c->device));
   const size_t wn = (size_t)n_ct * per_ct * all;
   DevBuf<uint64_t> dpv, dout;
   DevBuf<uint16_t> dpay, dw;
@@ -757,6 +670,7 @@ extern "C" omr_status omr_first_level(omr_ctx *c, const uint16_t *ca, const uint
   omr_status s;
   if ((s = stage_buffers(c, D)) != OMR_OK || (s = ensure_batch(c, D)) != OMR_OK) return s;
   hipStream_t st = c->stream;
+  if ((s = scratch_acquire(c, st)) != OMR_OK) return s;
   HIP_TRY(hipMemcpyAsync(c->s_clue_a, ca, D * N0 * sizeof(uint16_t), hipMemcpyHostToDevice, st));
   HIP_TRY(hipMemcpyAsync(c->s_clue_b, cb, D * CLUES * sizeof(uint16_t), hipMemcpyHostToDevice, st));
   const int B = (int)D;
@@ -771,6 +685,7 @@ extern "C" omr_status omr_first_level(omr_ctx *c, const uint16_t *ca, const uint
   }
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(lwe_int, c->lwe_int, D * (NI + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  if ((s = scratch_release(c, st)) != OMR_OK) return s;
   HIP_TRY(hipStreamSynchronize(st));
   return OMR_OK;
 }

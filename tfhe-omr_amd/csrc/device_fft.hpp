@@ -5,10 +5,8 @@
 // FFT product rounds to it exactly:
 //   level 1: |d| <= 17, |k| <= 2^26, 8 rows, N = 1024: |coef| < 2^43; worst error of a lane-exact
 //            model with adversarial digits 1.8e-3 (tools/fft_exactness.py), rigorous bound < 0.15;
-//   level 2: |d| <= 64, keys split in two 25-bit limbs |k_l| <= 2^24, 12 rows, N = 2048:
-//            |coef| < 2^44.6; worst adversarial error 2e-3 (tools/fft_exactness.py --level 2).
-// Replacing the modular NTTs by half-length complex FFTs removes ~45 % (level 1) and ~40 %
-// (level 2) of the FP64 work, with bit-identical results.
+// Replacing the modular NTTs by half-length complex FFTs removes ~45 % of the level-1 FP64 work,
+// with bit-identical results.
 //
 // Ring map: R[X]/(X^2n + 1) -> C[X]/(X^n - i), p -> z with z_j = p_j + i p_{j+n}, n = 2^L.
 // X^n - i splits over the roots w^(1+4k) (w = exp(i pi / 2n)); the forward transform is a
@@ -19,7 +17,7 @@
 //
 // T lanes hold E complex values each (N = T E), log2(E) radix-2 stages per pass, an LDS exchange
 // between passes (XOR swizzle found by tools/fft_lds_banks.py: no bank conflicts for
-// ds_write_b128 / ds_read_b128), C independent transforms interleaved.
+// ds_write_b128 / ds_read_b128), C independent transforms interleaved. One wave per transform.
 //   forward: in  x[e] = coefficient (lane + T e)    out x[e] = transform index (E lane + e)
 //   inverse: in  x[e] = transform index (E lane + e) out x[e] = coefficient (lane + T e)
 #pragma once
@@ -28,27 +26,12 @@
 
 #include "device_ntt.hpp"
 
-#ifndef OMR_FFT1_PAD_ADD
-#define OMR_FFT1_PAD_ADD 0  // level-1 FFT exchanges: additive padding (no spills, but slower: DESIGN §7)
-#endif
-
 namespace omr {
 
-#ifndef OMR_FFT_TW_PAIR
-#define OMR_FFT_TW_PAIR 1  // odd sibling nodes reuse the even node's twiddle (w_odd = i w_even)
-#endif
-#ifndef OMR_FFT_POSTREAD_WAIT
-#define OMR_FFT_POSTREAD_WAIT 0  // one-wave FFTs: lgkmcnt(0) after each exchange's reads (br1 +1.1 %: off)
-#endif
-#ifndef OMR_FFT_DB
-#define OMR_FFT_DB 1  // multi-wave FFTs: double-buffered, wave-local where the pass pair allows
-#endif
-
-// LDS visibility within one wave: keep the compiler from moving memory operations across (waves
-// of a workgroup stay independent). One wave's LDS instructions execute in issue order, so the
-// lgkmcnt wait is only needed with OMR_WAVE_SYNC_WAIT (the conservative form).
+// LDS visibility within one wave: this wave's LDS writes have landed, and the compiler moves no
+// memory operation across (waves of a workgroup stay independent).
 __device__ __forceinline__ void wave_lds_sync() {
-  if (OMR_WAVE_SYNC_WAIT) __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
   __builtin_amdgcn_wave_barrier();
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
 }
@@ -57,45 +40,20 @@ __device__ __forceinline__ void wave_lds_fence() {
   __builtin_amdgcn_wave_barrier();
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
 }
-// Transforms owned by one wave (T == 64) synchronise the wave only; larger ones the workgroup.
-template <int T>
-__device__ __forceinline__ void fft_sync() {
-  if constexpr (T == 64)
-    wave_lds_sync();
-  else
-    __syncthreads();
-}
-
-// LDS exchange layout per geometry. ADD: additive padding slot(j) = j + (j >> PS), separable
-// over the disjoint lane / element fields of an exchange index, so every access is one per-lane
-// base register plus an immediate offset (tools/fft_lds_pad.py: 96 extra conflict cycles over
-// all patterns for 64x8). Otherwise an XOR swizzle slot(j) = j ^ f(j) with no conflicts
-// (tools/fft_lds_banks.py), at the cost of per-element address registers.
+// XOR swizzle of the LDS exchange slots, slot(j) = j ^ f(j), f linear over GF(2): no bank
+// conflicts for any exchange of the geometry (tools/fft_lds_banks.py 64 8 9).
 template <int T, int E, int L>
 struct FftSwizzle;
 template <>
-struct FftSwizzle<64, 8, 9> {  // tools/fft_lds_banks.py 64 8 9; tools/fft_lds_pad.py 64 8 9
+struct FftSwizzle<64, 8, 9> {
   static constexpr int M[6] = {4, 9, 15, 14, 0, 8};
-  static constexpr bool ADD = OMR_FFT1_PAD_ADD != 0;
-  static constexpr int PS = 3;
-};
-template <>
-struct FftSwizzle<64, 16, 10> {  // tools/fft_lds_banks.py 64 16 10
-  static constexpr int M[7] = {3, 13, 14, 15, 6, 10, 15};
-  static constexpr bool ADD = false;
-  static constexpr int PS = 0;
-};
-template <>
-struct FftSwizzle<256, 4, 10> {  // tools/fft_lds_banks.py 256 4 10
-  static constexpr int M[7] = {2, 13, 6, 0, 4, 4, 2};
-  static constexpr bool ADD = false;
-  static constexpr int PS = 0;
 };
 
 template <int T_, int E_, int L_>
 struct WgFft {
   static constexpr int T = T_, E = E_, L = L_, N = T * E, R = ilog2(E), NPASS = (L + R - 1) / R;
   static_assert(N == (1 << L), "FFT geometry");
+  static_assert(T == 64, "one transform per wave (wave-level LDS synchronisation)");
   // stages in pass p (the last pass may be shorter)
   static constexpr int stages(int p) { return (L - p * R) < R ? (L - p * R) : R; }
 
@@ -113,21 +71,9 @@ struct WgFft {
   __device__ static __forceinline__ int swz(int j) {
     return j ^ swz_bits(j, std::make_integer_sequence<int, L - 3>{});
   }
-  static constexpr bool ADD = FftSwizzle<T, E, L>::ADD;
-  static constexpr int PS = FftSwizzle<T, E, L>::PS;
-  static constexpr int BUF = ADD ? N + (N >> PS) : N;  // LDS slots (double2) per transform
+  static constexpr int BUF = N;  // LDS slots (double2) per transform
   // slot of register e of `lane` in pass p
-  __device__ static __forceinline__ int slot(int p, int lane, int e) {
-    if constexpr (ADD) {
-      static_assert(L % R == 0, "additive layout written for full passes");
-      const int lb = L - (p + 1) * R;
-      const int lp = ((lane >> lb) << (L - p * R)) | (lane & ((1 << lb) - 1));
-      const int ep = e << lb;
-      return (lp + (lp >> PS)) + (ep + (ep >> PS));  // = j + (j >> PS), fields disjoint
-    } else {
-      return swz(index(p, lane, e));
-    }
-  }
+  __device__ static __forceinline__ int slot(int p, int lane, int e) { return swz(index(p, lane, e)); }
   // Node twiddle of stage P*R + k for register e. The last pass's stages are stored lane-minor
   // (entry (1 << s) + j * T + lane holds node (lane << k) + j) so a wave reads consecutive
   // entries; in earlier passes lanes of a group share (broadcast) entries.
@@ -143,68 +89,27 @@ struct WgFft {
     return (1 << (s0 + k)) + node;
   }
 
-  // lane owning element idx in pass p (inverse of index())
-  static constexpr int thread_of(int p, int idx) {
-    const int s0 = p * R, r = stages(p), lb = L - s0 - r;
-    const int F = ((idx >> (L - s0)) << lb) | (idx & ((1 << lb) - 1));
-    return F >> (R - r);
-  }
-  // every element stays in its wave between passes pf and pt (the swizzle keeps the bits above
-  // the low four, so each wave then reads and writes only its own slots)
-  static constexpr bool wave_local(int pf, int pt) {
-    if (T <= 64) return true;
-    for (int idx = 0; idx < N; ++idx)
-      if ((thread_of(pf, idx) >> 6) != (thread_of(pt, idx) >> 6)) return false;
-    return true;
-  }
-  // Multi-wave single transforms alternate two LDS buffers (lds then holds 2 * BUF): only the
-  // transform's last exchange needs a barrier after its reads.
-  static constexpr bool DB = T > 64 && OMR_FFT_DB != 0;
-
-  // Exchange PF -> PT, the ORD-th of the transform. LAST: no exchange of this transform follows.
-  // PREV_WL: the previous exchange was wave-local (other waves may still read their slots).
-  template <int C, int PF, int PT, int ORD, bool LAST, bool PREV_WL>
+  // Exchange between passes PF and PT through the wave's LDS buffer (C transforms).
+  template <int C, int PF, int PT>
   __device__ static __forceinline__ void exchange(double (&xr)[C][E], double (&xi)[C][E],
                                                   double2 *lds, int lane) {
-#ifdef OMR_EXPT_NO_EXCH  // timing experiment only (wrong results): no LDS exchange
-    return;
-#endif
-    constexpr bool WL = wave_local(PF, PT);
-    constexpr bool db = DB && C == 1;
-    if constexpr (T > 64 && !WL && PREV_WL) __syncthreads();
-    double2 *buf = lds + (db ? (ORD & 1) * BUF : 0);
 #pragma unroll
     for (int c = 0; c < C; ++c)
 #pragma unroll
       for (int e = 0; e < E; ++e)
-        buf[c * BUF + slot(PF, lane, e)] = make_double2(xr[c][e], xi[c][e]);
-    if constexpr (WL)
-      wave_lds_sync();
-    else
-      __syncthreads();
+        lds[c * BUF + slot(PF, lane, e)] = make_double2(xr[c][e], xi[c][e]);
+    wave_lds_sync();
 #pragma unroll
     for (int c = 0; c < C; ++c)
 #pragma unroll
       for (int e = 0; e < E; ++e) {
-        const double2 v = buf[c * BUF + slot(PT, lane, e)];
+        const double2 v = lds[c * BUF + slot(PT, lane, e)];
         xr[c][e] = v.x;
         xi[c][e] = v.y;
       }
-    if constexpr (T <= 64) {
-      // the next exchange's writes must not move above these reads: a compiler fence suffices
-      // (one wave's LDS operations complete in order); OMR_FFT_POSTREAD_WAIT also waits for them
-      if (OMR_FFT_POSTREAD_WAIT) {
-        wave_lds_sync();
-      } else {
-        __builtin_amdgcn_wave_barrier();
-        __atomic_signal_fence(__ATOMIC_SEQ_CST);
-      }
-    } else if constexpr (LAST || !db) {
-      if constexpr (!LAST && WL)
-        wave_lds_sync();
-      else
-        __syncthreads();
-    }
+    // the next exchange's writes must not move above these reads: a compiler fence suffices
+    // (one wave's LDS operations complete in order; waiting for the reads here is 1.1 % slower)
+    wave_lds_fence();
   }
 
   // Pass 0's node index does not depend on the lane (lane >> (L - R) == 0), so its twiddles
@@ -214,9 +119,6 @@ struct WgFft {
   __device__ static __forceinline__ double2 twiddle(const double2 *tws, const double2 *__restrict__ gtw,
                                                     int k, int e, int lane) {
     if constexpr (P == 0 && G) return gtw[(1 << k) + ((e & ((1 << stages(0)) - 1)) >> (stages(0) - k))];
-#ifdef OMR_EXPT_TW_CONST  // timing experiment only (wrong results): no twiddle loads
-    return make_double2(0.70710678118654752 + k, 0.70710678118654752 - e);
-#endif
     return tws[twiddle_index<P>(k, e, lane)];
   }
 
@@ -235,7 +137,7 @@ struct WgFft {
         // sibling nodes 2j, 2j + 1 have twiddles w and i w (half-angles of eps and eps + 2n):
         // odd nodes reuse the even twiddle and apply the factor i by swapping parts (fewer LDS
         // twiddle reads, no extra arithmetic)
-        const int pb = (OMR_FFT_TW_PAIR && k >= 1) ? (1 << (r - k)) : 0;
+        const int pb = k >= 1 ? (1 << (r - k)) : 0;
         const bool odd = (e & pb) != 0;
         const double2 w = twiddle<P, G>(tws, gtw, k, odd ? (e & ~pb) : e, lane);
 #pragma unroll
@@ -262,7 +164,7 @@ struct WgFft {
 #pragma unroll
       for (int e = 0; e < E; ++e) {
         if (e & half) continue;
-        const int pb = (OMR_FFT_TW_PAIR && k >= 1) ? (1 << (r - k)) : 0;  // see fwd_pass
+        const int pb = k >= 1 ? (1 << (r - k)) : 0;  // see fwd_pass
         const bool odd = (e & pb) != 0;
         const double2 w = twiddle<P, G>(tws, gtw, k, odd ? (e & ~pb) : e, lane);
 #pragma unroll
@@ -290,32 +192,8 @@ struct WgFft {
 #define OMR_FFT_FWD_STEP(P)                                                                   \
   if constexpr (NPASS > P) {                                                                  \
     constexpr int Q = NPASS > P ? P : 1;                                                      \
-    exchange<C, Q - 1, Q, Q - 1, Q == NPASS - 1, (Q >= 2) && wave_local(Q >= 2 ? Q - 2 : 0, Q - 1)>( \
-        xr, xi, lds, lane);                                                                   \
+    exchange<C, Q - 1, Q>(xr, xi, lds, lane);                                                 \
     fwd_pass<(NPASS > P ? P : 0), C>(xr, xi, tws, lane);                                      \
-  }
-    OMR_FFT_FWD_STEP(1)
-    OMR_FFT_FWD_STEP(2)
-    OMR_FFT_FWD_STEP(3)
-    OMR_FFT_FWD_STEP(4)
-#undef OMR_FFT_FWD_STEP
-  }
-  // Forward transform calling hook(p) after the compute of pass p (p = 0 .. NPASS - 1): lets a
-  // caller spread independent work (e.g. LDS-DMA issues) over the transform's VALU phases.
-  template <int C, bool G, class Hook>
-  __device__ static __forceinline__ void fwd_hooked(double (&xr)[C][E], double (&xi)[C][E], double2 *lds,
-                                                    const double2 *tws, int lane,
-                                                    const double2 *__restrict__ gtw, Hook &&hook) {
-    static_assert(NPASS <= 5, "unrolled for up to 5 passes");
-    fwd_pass<0, C, G>(xr, xi, tws, lane, gtw);
-    hook(0);
-#define OMR_FFT_FWD_STEP(P)                                                                   \
-  if constexpr (NPASS > P) {                                                                  \
-    constexpr int Q = NPASS > P ? P : 1;                                                      \
-    exchange<C, Q - 1, Q, Q - 1, Q == NPASS - 1, (Q >= 2) && wave_local(Q >= 2 ? Q - 2 : 0, Q - 1)>( \
-        xr, xi, lds, lane);                                                                   \
-    fwd_pass<(NPASS > P ? P : 0), C>(xr, xi, tws, lane);                                      \
-    hook(P);                                                                                  \
   }
     OMR_FFT_FWD_STEP(1)
     OMR_FFT_FWD_STEP(2)
@@ -332,8 +210,7 @@ struct WgFft {
   if constexpr (NPASS > P) {                                                                  \
     constexpr int Q = NPASS > P ? P : 1;                                                      \
     inv_pass<(NPASS > P ? P : 0), C>(xr, xi, tws, lane);                                      \
-    exchange<C, Q, Q - 1, NPASS - 1 - Q, Q == 1,                                              \
-             (Q + 1 <= NPASS - 1) && wave_local(Q + 1 <= NPASS - 1 ? Q + 1 : Q, Q)>(xr, xi, lds, lane); \
+    exchange<C, Q, Q - 1>(xr, xi, lds, lane);                                                 \
   }
     OMR_FFT_INV_STEP(4)
     OMR_FFT_INV_STEP(3)
@@ -354,8 +231,6 @@ struct WgFft {
   }
 };
 
-using Fft512 = WgFft<64, 8, 9>;     // level 1: N1 = 1024, one wave
-using Fft1024 = WgFft<256, 4, 10>;  // level 2: N2 = 2048, four waves
-using Fft1024W = WgFft<64, 16, 10>; // level 2: N2 = 2048, one wave (16 points per lane)
+using Fft512 = WgFft<64, 8, 9>;  // level 1: N1 = 1024, one wave
 
 }  // namespace omr

@@ -10,34 +10,6 @@
 
 #include "common.hpp"
 
-#ifndef OMR_NTT_WAVE_LOCAL
-#define OMR_NTT_WAVE_LOCAL 1  // wave-level sync for NTT exchanges that stay inside each wave
-#endif
-#ifndef OMR_WAVE_SYNC_WAIT
-#define OMR_WAVE_SYNC_WAIT 1  // wave-local exchanges wait for the wave's own LDS writes
-#endif
-#ifndef OMR_CANON_RED
-#define OMR_CANON_RED 1  // canonical residues by a second rounded reduction (no VCC selects)
-#endif
-#ifndef OMR_XBUF3
-#define OMR_XBUF3 1  // level-2 blind rotation: three-buffer exchanges, one barrier per transform
-#endif
-#ifndef OMR_NTT_SMALL0
-#define OMR_NTT_SMALL0 1  // level 2: inverse twiddles mirrored from the forward table, stage-0 digit table
-#endif
-#ifndef OMR_NTT_T0
-#define OMR_NTT_T0 2  // small-digit level-2 NTTs: 2 stages 0 and 1 from five LDS tables (-1.4 %),
-                      // 1 stage-0 products d * tw[1] from one table, 0 computed (+2 %)
-#endif
-#if OMR_NTT_T0 == 2
-#define OMR_NTT_T0_TABLES 5
-#else
-#define OMR_NTT_T0_TABLES 1
-#endif
-#ifndef OMR_DB_XCH
-#define OMR_DB_XCH 1  // NTT exchanges through two alternating LDS buffers (fewer barriers)
-#endif
-
 namespace omr {
 
 template <int LEVEL>
@@ -77,23 +49,16 @@ __device__ __forceinline__ double red(double x) {
 // errs by far less than the 2^-52 gap between (q +- 1) / 2q and 1/2, so rint picks the right
 // quotient at the +-(q-1)/2 boundaries (checked for both primes). red(red(x)) therefore
 // canonicalises any |x| < 2^53 (red leaves |r| <= q/2 + 2) without compare/select pairs, which
-// serialise on VCC with hazard NOPs (OMR_CANON_RED = 0 keeps the select form).
+// serialise on VCC with hazard NOPs.
 // exact centred representative in [-(q-1)/2, (q-1)/2]
 template <class M>
 __device__ __forceinline__ double canon(double x) {
-  double r = red<M>(x);
-  if (OMR_CANON_RED) return red<M>(r);
-  r = r > M::HALF ? r - M::Q : r;
-  r = r < -M::HALF ? r + M::Q : r;
-  return r;
+  return red<M>(red<M>(x));
 }
 // for |x| <= q - 1 (sum/difference of two canonical values)
 template <class M>
 __device__ __forceinline__ double canon_small(double x) {
-  if (OMR_CANON_RED) return red<M>(x);
-  x = x > M::HALF ? x - M::Q : x;
-  x = x < -M::HALF ? x + M::Q : x;
-  return x;
+  return red<M>(x);
 }
 template <class M>
 __device__ __forceinline__ uint64_t to_u64(double c) {  // canonical centred -> [0, q)
@@ -124,9 +89,8 @@ struct WgNtt {
   static constexpr int NPASS = (L + R - 1) / R;
   static_assert(N == M::N, "NTT size mismatch");
   // Exchanges alternate between two LDS buffers so only the last exchange of a transform needs
-  // the barrier after its reads (DB); lds then holds 2 * C * N doubles.
-  static constexpr bool DB = OMR_DB_XCH != 0;
-  static constexpr int LDS_DOUBLES = (DB ? 2 : 1) * N;
+  // the barrier after its reads; lds then holds 2 * C * N doubles.
+  static constexpr int LDS_DOUBLES = 2 * N;
 
   // XOR swizzle of the exchange buffer: bank-conflict free for every (T, E) used here
   // (tools/lds_banks.py models the ds_read_b64 / ds_write_b64 lane groups).
@@ -166,7 +130,7 @@ struct WgNtt {
     return true;
   }
   __device__ static __forceinline__ void wave_sync() {
-    if (OMR_WAVE_SYNC_WAIT) __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0), see wave_lds_sync
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes have landed
     __builtin_amdgcn_wave_barrier();
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
   }
@@ -177,12 +141,9 @@ struct WgNtt {
   // reading their own slots; a cross-wave exchange must then wait for all of them first.
   template <int C, int PF, int PT, int ORD, bool LAST, bool PREV_WL>
   __device__ static __forceinline__ void exchangeC(double (&x)[C][E], double *lds, int tid) {
-#ifdef OMR_EXPT_NTT_NO_EXCH  // timing experiment only (wrong results)
-    return;
-#endif
-    constexpr bool WL = wave_local(PF, PT) && OMR_NTT_WAVE_LOCAL;
-    if constexpr (!WL && PREV_WL && OMR_NTT_WAVE_LOCAL) __syncthreads();
-    double *buf = lds + (DB ? (ORD & 1) * C * N : 0);
+    constexpr bool WL = wave_local(PF, PT);
+    if constexpr (!WL && PREV_WL) __syncthreads();
+    double *buf = lds + (ORD & 1) * C * N;
 #pragma unroll
     for (int c = 0; c < C; ++c)
 #pragma unroll
@@ -195,7 +156,7 @@ struct WgNtt {
     for (int c = 0; c < C; ++c)
 #pragma unroll
       for (int e = 0; e < E; ++e) x[c][e] = buf[c * N + pad(index(PT, tid, e))];
-    if constexpr (LAST || !DB) {
+    if constexpr (LAST) {
       if constexpr (!LAST && WL)
         wave_sync();
       else
@@ -203,10 +164,10 @@ struct WgNtt {
     }
   }
 
-  // G: pass 0's twiddles (wave-uniform: hi == 0) come from the global table gtw by scalar loads
-  template <int P, int C, bool G = false, int K0 = 0>
+  // K0: first stage of the pass (a caller that computed the earlier stages itself)
+  template <int P, int C, int K0 = 0>
   __device__ static __forceinline__ void fwd_passC(double (&x)[C][E], const double *tw, int tid,
-                                                   int &since_red, const double *__restrict__ gtw = nullptr) {
+                                                   int &since_red) {
     constexpr int s0 = P * R;
     constexpr int r = (L - s0) < R ? (L - s0) : R;
     constexpr int lb = L - s0 - r;
@@ -225,12 +186,7 @@ struct WgNtt {
         if (ep & half) continue;
         const int F = (tid << (R - r)) | (e >> r);
         const int hi = F >> lb;
-#ifdef OMR_EXPT_NTT_TW_CONST  // timing experiment only (wrong results)
-        const double w = 1234567.0 + s * 3 + e;
-#else
-        const double w = (P == 0 && G) ? gtw[(1 << s) + (ep >> (r - k))]
-                                       : tw[(1 << s) + ((hi << k) | (ep >> (r - k)))];
-#endif
+        const double w = tw[(1 << s) + ((hi << k) | (ep >> (r - k)))];
 #pragma unroll
         for (int c = 0; c < C; ++c) {
           const double u = x[c][e];
@@ -246,9 +202,9 @@ struct WgNtt {
   // MIRROR: itw is the FORWARD table: psi^-brv(2^s + j) = -psi^brv(2^(s+1) - 1 - j) (the node's
   // mirror in its stage), so w = tw[2^(s+1) - 1 - node] and the butterfly multiplies (v - u)
   // instead of (u - v) -- the same exact product, and no inverse table in LDS.
-  template <int P, int C, bool G = false, bool MIRROR = false>
+  template <int P, int C, bool MIRROR = false>
   __device__ static __forceinline__ void inv_passC(double (&x)[C][E], const double *itw, int tid,
-                                                   int &since_red, const double *__restrict__ gitw = nullptr) {
+                                                   int &since_red) {
     constexpr int s0 = P * R;
     constexpr int r = (L - s0) < R ? (L - s0) : R;
     constexpr int lb = L - s0 - r;
@@ -267,13 +223,8 @@ struct WgNtt {
         if (ep & half) continue;
         const int F = (tid << (R - r)) | (e >> r);
         const int hi = F >> lb;
-#ifdef OMR_EXPT_NTT_TW_CONST  // timing experiment only (wrong results)
-        const double w = 7654321.0 + s * 3 + e;
-#else
         const int node = (hi << k) | (ep >> (r - k));
-        const double w = (P == 0 && G) ? gitw[(1 << s) + (ep >> (r - k))]
-                                       : (MIRROR ? itw[(2 << s) - 1 - node] : itw[(1 << s) + node]);
-#endif
+        const double w = MIRROR ? itw[(2 << s) - 1 - node] : itw[(1 << s) + node];
 #pragma unroll
         for (int c = 0; c < C; ++c) {
           const double u = x[c][e];
@@ -286,26 +237,24 @@ struct WgNtt {
     }
   }
 
-  template <int P, int C, bool G = false>
+  template <int P, int C>
   __device__ static __forceinline__ void fwd_fromC(double (&x)[C][E], double *lds, const double *tw,
-                                                   int tid, int &since_red,
-                                                   const double *__restrict__ gtw = nullptr) {
+                                                   int tid, int &since_red) {
     if constexpr (P < NPASS) {
       if constexpr (P > 0)
         exchangeC<C, P - 1, P, P - 1, P == NPASS - 1, (P >= 2) && wave_local(P - 2, P - 1)>(x, lds, tid);
-      fwd_passC<P, C, G>(x, tw, tid, since_red, gtw);
-      fwd_fromC<P + 1, C, G>(x, lds, tw, tid, since_red, gtw);
+      fwd_passC<P, C>(x, tw, tid, since_red);
+      fwd_fromC<P + 1, C>(x, lds, tw, tid, since_red);
     }
   }
-  template <int P, int C, bool G = false>
+  template <int P, int C>
   __device__ static __forceinline__ void inv_fromC(double (&x)[C][E], double *lds, const double *itw,
-                                                   int tid, int &since_red,
-                                                   const double *__restrict__ gitw = nullptr) {
+                                                   int tid, int &since_red) {
     if constexpr (P >= 0) {
       if constexpr (P < NPASS - 1)
         exchangeC<C, P + 1, P, NPASS - 2 - P, P == 0, (P + 2 <= NPASS - 1) && wave_local(P + 2, P + 1)>(x, lds, tid);
-      inv_passC<P, C, G>(x, itw, tid, since_red, gitw);
-      inv_fromC<P - 1, C, G>(x, lds, itw, tid, since_red, gitw);
+      inv_passC<P, C>(x, itw, tid, since_red);
+      inv_fromC<P - 1, C>(x, lds, itw, tid, since_red);
     }
   }
 
@@ -323,22 +272,7 @@ struct WgNtt {
     inv_fromC<NPASS - 1, C>(x, lds, itw, tid, since_red);
   }
 
-  // Single transforms with pass 0's twiddles from the global tables (scalar loads): pass 0 has
-  // hi == 0 for every thread (T = 2^(L - R)), so its 2^R - 1 twiddles are workgroup-uniform.
-  __device__ static __forceinline__ void fwd_g(double (&x)[E], double *lds, const double *tw,
-                                               const double *__restrict__ gtw, int tid) {
-    static_assert(T == (1 << (L - R)), "pass-0 twiddles uniform only for a full first pass");
-    int since_red = 0;
-    fwd_fromC<0, 1, true>(reinterpret_cast<double(&)[1][E]>(x), lds, tw, tid, since_red, gtw);
-  }
-  __device__ static __forceinline__ void inv_g(double (&x)[E], double *lds, const double *itw,
-                                               const double *__restrict__ gitw, int tid) {
-    static_assert(T == (1 << (L - R)), "pass-0 twiddles uniform only for a full first pass");
-    int since_red = 0;
-    inv_fromC<NPASS - 1, 1, true>(reinterpret_cast<double(&)[1][E]>(x), lds, itw, tid, since_red, gitw);
-  }
-
-  // ---- three-buffer single transforms (OMR_XBUF3) -------------------------------------------
+  // ---- three-buffer single transforms (level-2 CMUX step) -------------------------------------------
   // Cross-wave exchanges use X0 = lds or X1 = lds + N as the caller chooses (XB), wave-local ones
   // W = lds + 2N, where each wave only ever touches its own slots (the index set a wave owns in
   // a wave-local pass pair is the same for every such pair). A caller that alternates X0 / X1
@@ -382,51 +316,37 @@ struct WgNtt {
                                                    int tid, int &since_red) {
     if constexpr (P >= 0) {
       if constexpr (P < NPASS - 1) exchange3<P + 1, P, XB>(x, lds, tid);
-      inv_passC<P, 1, false, MIRROR>(reinterpret_cast<double(&)[1][E]>(x), itw, tid, since_red);
+      inv_passC<P, 1, MIRROR>(reinterpret_cast<double(&)[1][E]>(x), itw, tid, since_red);
       inv3_from<P - 1, XB, MIRROR>(x, lds, itw, tid, since_red);
     }
   }
-  // Forward transform of a polynomial of small integer digits |d| <= 64: stage 0 (pairs e,
-  // e + E/2, twiddle tw[1] for every thread) takes d * tw[1] mod q from the 129-entry table t0
-  // (t0[d + 64], centred) instead of a modular product; with OMR_NTT_T0 = 2 stage 1 too.
+  // Forward transform of a polynomial of small integer digits |d| <= 64: stages 0 and 1 from
+  // five 129-entry LDS tables (t0 + 136 k: d * c_k for c = tw1, tw2, tw1 tw2, tw3, tw1 tw3)
+  // instead of modular products. Stage 0 pairs (e, e + 4) under tw[1] for every thread; stage 1
+  // pairs (e, e + 2) with tw[2] (e = 0, 1) and tw[3] (e = 4, 5), so tw2 * x[2] = tw2 d2 +
+  // tw1 tw2 d6 and tw3 * x[6] = tw3 d2 - tw1 tw3 d6 are table sums. Bound: |x| <= 2q after stage 1
+  // (1.7q with the products), 6.84q before the stage-6 reduction: below 8q < 2^53 and inside mm's
+  // exact range (replayed in tests/test_fp64_residues.py).
   template <int XB>
   __device__ static __forceinline__ void fwd3_small(const int (&d)[E], const double *t0, double (&x)[E],
                                                     double *lds, const double *tw, int tid) {
-    static_assert(R == 3 && T == (1 << (L - R)), "stage-0 table written for full radix-8 first passes");
-    if constexpr (OMR_NTT_T0 == 2) {
-      // stages 0 and 1 from five tables (t0 + 136 k: d * c_k for c = tw1, tw2, tw1 tw2, tw3,
-      // tw1 tw3). Stage 1 pairs (e, e + 2) with tw[2] (e = 0, 1) and tw[3] (e = 4, 5), so
-      // tw2 * x[2] = tw2 d2 + tw1 tw2 d6 and tw3 * x[6] = tw3 d2 - tw1 tw3 d6 are table sums.
-      // Bound: |x| <= 2q after stage 1 (1.7q with the products), 6.84q before the stage-6
-      // reduction: below 8q < 2^53 and inside mm's exact range.
-      const double *T1 = t0, *T2 = t0 + 136, *T3 = t0 + 272, *T4 = t0 + 408, *T5 = t0 + 544;
-      const double a4 = T1[d[4] + 64], a5 = T1[d[5] + 64];
-      const double x0 = (double)d[0] + a4, x4 = (double)d[0] - a4;
-      const double x1 = (double)d[1] + a5, x5 = (double)d[1] - a5;
-      const double v0 = T2[d[2] + 64] + T3[d[6] + 64], v1 = T2[d[3] + 64] + T3[d[7] + 64];
-      const double v4 = T4[d[2] + 64] - T5[d[6] + 64], v5 = T4[d[3] + 64] - T5[d[7] + 64];
-      x[0] = x0 + v0;
-      x[2] = x0 - v0;
-      x[1] = x1 + v1;
-      x[3] = x1 - v1;
-      x[4] = x4 + v4;
-      x[6] = x4 - v4;
-      x[5] = x5 + v5;
-      x[7] = x5 - v5;
-      int since_red = 2;
-      fwd_passC<0, 1, false, 2>(reinterpret_cast<double(&)[1][E]>(x), tw, tid, since_red);
-      fwd3_from<1, XB>(x, lds, tw, tid, since_red);
-      return;
-    }
-#pragma unroll
-    for (int e = 0; e < E / 2; ++e) {
-      const double u = (double)d[e];
-      const double v = OMR_NTT_T0 ? t0[d[e + E / 2] + 64] : mm<M>((double)d[e + E / 2], tw[1]);
-      x[e] = u + v;
-      x[e + E / 2] = u - v;
-    }
-    int since_red = 1;
-    fwd_passC<0, 1, false, 1>(reinterpret_cast<double(&)[1][E]>(x), tw, tid, since_red);
+    static_assert(R == 3 && T == (1 << (L - R)), "stage tables written for full radix-8 first passes");
+    const double *T1 = t0, *T2 = t0 + 136, *T3 = t0 + 272, *T4 = t0 + 408, *T5 = t0 + 544;
+    const double a4 = T1[d[4] + 64], a5 = T1[d[5] + 64];
+    const double x0 = (double)d[0] + a4, x4 = (double)d[0] - a4;
+    const double x1 = (double)d[1] + a5, x5 = (double)d[1] - a5;
+    const double v0 = T2[d[2] + 64] + T3[d[6] + 64], v1 = T2[d[3] + 64] + T3[d[7] + 64];
+    const double v4 = T4[d[2] + 64] - T5[d[6] + 64], v5 = T4[d[3] + 64] - T5[d[7] + 64];
+    x[0] = x0 + v0;
+    x[2] = x0 - v0;
+    x[1] = x1 + v1;
+    x[3] = x1 - v1;
+    x[4] = x4 + v4;
+    x[6] = x4 - v4;
+    x[5] = x5 + v5;
+    x[7] = x5 - v5;
+    int since_red = 2;
+    fwd_passC<0, 1, 2>(reinterpret_cast<double(&)[1][E]>(x), tw, tid, since_red);
     fwd3_from<1, XB>(x, lds, tw, tid, since_red);
   }
   // Inverse with the forward table mirrored (MIRROR in inv_passC): tw is the forward table.
@@ -436,20 +356,6 @@ struct WgNtt {
     int since_red = 0;
     inv3_from<NPASS - 1, XB, true>(x, lds, tw, tid, since_red);
   }
-  // XB: the cross-wave buffer (0 / 1) this transform's single cross-wave exchange uses
-  template <int XB>
-  __device__ static __forceinline__ void fwd3(double (&x)[E], double *lds, const double *tw, int tid) {
-    static_assert(cross_wave_exchanges() == 1, "three-buffer scheme written for one cross-wave exchange");
-    int since_red = 0;
-    fwd3_from<0, XB>(x, lds, tw, tid, since_red);
-  }
-  template <int XB>
-  __device__ static __forceinline__ void inv3(double (&x)[E], double *lds, const double *itw, int tid) {
-    static_assert(cross_wave_exchanges() == 1, "three-buffer scheme written for one cross-wave exchange");
-    int since_red = 0;
-    inv3_from<NPASS - 1, XB>(x, lds, itw, tid, since_red);
-  }
-
   // Single-transform API.
   __device__ static __forceinline__ void fwd(double (&x)[E], double *lds, const double *tw, int tid) {
     fwdC<1>(reinterpret_cast<double(&)[1][E]>(x), lds, tw, tid);

@@ -132,15 +132,19 @@ __global__ __launch_bounds__(ENC_T) void encode_payloads_kernel(
   }
 }
 
-// out[c][t] = sum_chunk partial[c][chunk][t] mod q2 (chunks < 2^13 keeps the u64 sum exact).
+// out[c][t] = sum_chunk partial[c][chunk][t] mod q2: every partial is canonical (< q2), so the
+// running sum stays canonical with one conditional subtraction per term, for any chunk count.
 __global__ void reduce_partials_kernel(const uint64_t *__restrict__ partial, int chunks,
                                        int n_ct, uint64_t *__restrict__ out) {
   const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= (size_t)n_ct * 2 * N2) return;
   const size_t c = idx / (2 * N2), t = idx % (2 * N2);
   uint64_t s = 0;
-  for (int k = 0; k < chunks; ++k) s += partial[((size_t)c * chunks + k) * 2 * N2 + t];
-  out[idx] = s % Q2;
+  for (int k = 0; k < chunks; ++k) {
+    s += partial[((size_t)c * chunks + k) * 2 * N2 + t];
+    s = s >= Q2 ? s - Q2 : s;
+  }
+  out[idx] = s;
 }
 
 }  // namespace omr

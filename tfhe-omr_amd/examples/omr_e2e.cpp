@@ -1,4 +1,4 @@
-// omr_e2e — the reference's end-to-end example (omr_core/examples/omr.rs:94-293) driven through
+// omr_e2e — the reference's end-to-end example (omr_core/examples/omr.rs:30-235) driven through
 // the C ABI of include/omr_gpu.h from native code: key generation, clue generation (pertinent
 // messages from sender A, the rest from sender B), detect on the GPU, encode_pertinent_indices /
 // encode_pertinent_payloads, client-side retrieval, and a check that exactly the pertinent
@@ -68,7 +68,7 @@ int main(int argc, char **argv) {
   CHECK(omr_keygen_detection_key(pa, seed ^ 0xD, bsk1.data(), ksk.data(), bsk2.data(), tk.data(), 0));
   std::printf("keygen time: %.3f s\n", secs(t));
 
-  // pertinent = first min(D, 50) of a shuffle (omr.rs:102-113)
+  // pertinent = first min(D, 50) of a shuffle (omr.rs:103-113)
   const size_t pert_count = std::min<size_t>(D, 50);
   std::vector<size_t> order(D);
   std::iota(order.begin(), order.end(), 0);
@@ -79,7 +79,7 @@ int main(int argc, char **argv) {
   std::vector<char> is_pert(D, 0);
   for (size_t i : pert) is_pert[i] = 1;
 
-  // Sender::gen_clues for every message (omr.rs:124-135)
+  // Sender::gen_clues for every message (omr.rs:126-135)
   t = clk::now();
   std::vector<uint16_t> ca(D * N0), cb(D * CLUES), xa(D * N0), xb(D * CLUES);
   CHECK(omr_gen_clues(pa, seed + 1, 0, D, ca.data(), cb.data(), 0));
@@ -91,7 +91,7 @@ int main(int argc, char **argv) {
     }
   std::printf("gen clues time: %.3f s\n", secs(t));
 
-  // Payload::random (omr.rs:138-145)
+  // Payload::random (omr.rs:140-146)
   std::vector<uint16_t> payloads(D * PAYLOAD);
   for (auto &b : payloads) b = (uint16_t)(rng() & 0xff);
 
@@ -111,7 +111,7 @@ int main(int argc, char **argv) {
     return 0;
   }
 
-  // Detector::new + detect over the board (omr.rs:160-178)
+  // Detector::new + detect over the board (omr.rs:160-164)
   omr_ctx *ctx = nullptr;
   omr_detection_key_view view{bsk1.data(), ksk.data(), bsk2.data(), tk.data()};
   CHECK(omr_ctx_create(&view, device, &ctx));
@@ -133,7 +133,7 @@ int main(int argc, char **argv) {
                             rp.cmb_count_per_cipher, pay_ct.data()));
   std::printf("encode pertinent payloads time: %.3f s\n", secs(t));
 
-  // Retriever::decode_digest (omr.rs:266-275)
+  // Retriever::decode_digest (omr.rs:216-218)
   t = clk::now();
   std::vector<size_t> found(pert_count + 64);
   size_t nfound = 0;

@@ -2,20 +2,23 @@
 "nccl" backend is RCCL over xGMI on MI355X), messages sharded by contiguous global-index
 ranges, no data-path collective for detect, and one reduce of the partial digests.
 
-Reference behaviour (examples/omr.rs:154-293): detect every message (:219-223), then
-encode_pertinent_indices for each index ciphertext (:239-242) and encode_pertinent_payloads
-once (:256-262) over the WHOLE board. Encoding is linear in the pertinency vector, so each
-rank encodes its own range with global indices and the partial digests are summed mod q2.
-The bucket choices and payload weights are functions of (seed, global index), so the
-result is independent of the number of ranks.
+Reference behaviour (examples/omr.rs): detect every message (`par_iter().map(detect)`,
+:160-164), then encode_pertinent_indices for each index ciphertext and
+encode_pertinent_payloads once over the WHOLE board (:180-203). Encoding is linear in the
+pertinency vector, so each rank encodes its own range with global indices and the partial
+digests are summed mod q2. The bucket choices and payload weights are functions of (seed,
+global index), so the result is independent of the number of ranks.
 
-The compute backend is any object with `detect_batch(clue_a, clue_b)`,
-`encode_pertinent_indices(rp, pv, seed, ct, global_offset)` and
-`encode_pertinent_payloads(pv, payloads, weights, rp, global_offset)` — the GPU `Detector`
-in production; tests also plug in the CPU oracle to exercise the orchestration under gloo.
+bench.py and tests/test_dist_gloo.py both drive `run_omr_shard` / `encode_and_reduce`; the
+compute backend is `GpuBackend` (libomr_gpu.so on device buffers) in production, and a CPU
+oracle backend in the gloo test. A backend provides:
+    detect(clue_a, clue_b) -> pertinency vector (backend-native buffer, D x 2 x 2048)
+    encode(pv, payloads, first, total, rp, index_seed, weights) -> torch.int64 tensor
+        [n_idx + n_pay][2][2048] of canonical partial digests (index ciphertexts first)
 """
 from __future__ import annotations
 
+import time
 from dataclasses import dataclass
 
 import numpy as np
@@ -30,42 +33,108 @@ def shard_range(rank: int, world: int, total: int) -> tuple[int, int]:
     return first, base + (1 if rank < rem else 0)
 
 
+def plan(rank: int, world: int, per_gpu: int | None = None, total: int | None = None):
+    """(first, count, total) of this rank. Weak scaling: `per_gpu` messages on every rank
+    (total = per_gpu * world). Strong scaling: `total` messages split over the ranks."""
+    if (per_gpu is None) == (total is None):
+        raise ValueError("give exactly one of per_gpu (weak scaling) or total (strong scaling)")
+    if per_gpu is not None:
+        return rank * per_gpu, per_gpu, per_gpu * world
+    first, count = shard_range(rank, world, total)
+    return first, count, total
+
+
 @dataclass
 class Digest:
     indices: np.ndarray   # u64 [n_idx_ct][2][2048]
     payloads: np.ndarray  # u64 [n_pay_ct][2][2048]
 
 
-def reduce_digest(local: np.ndarray, dist=None, device=None, dst: int = 0) -> np.ndarray | None:
-    """Sum partial digests over ranks (int64; each < q2 < 2^50, <= 8192 ranks stay exact) and
-    reduce mod q2 on `dst`. Returns the digest on dst, None elsewhere."""
+def reduce_digest(local, dist=None, dst: int = 0):
+    """Sum the partial digests (torch.int64 [n_ct][2][2048], canonical < q2 < 2^50; the int64
+    sum is exact up to 8,192 ranks) over the ranks with one reduce, and reduce mod q2 on `dst`.
+    Returns the digest (numpy u64) on dst, None elsewhere. `local` lives where the process
+    group's backend wants it (device memory for RCCL, host memory for gloo)."""
+    if dist is not None and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.reduce(local, dst=dst, op=dist.ReduceOp.SUM)
+        if dist.get_rank() != dst:
+            return None
+    return local.cpu().numpy().view(np.uint64) % np.uint64(Q2)
+
+
+def encode_and_reduce(backend, pv, payloads, first: int, total: int, rp, index_seed: int, weights,
+                      dist=None, dst: int = 0):
+    """encode_pertinent_indices (every index ciphertext) + encode_pertinent_payloads over this
+    rank's shard with global indices, then the digest reduce. Returns (Digest or None on the
+    other ranks, {"encode_s", "encode_reduce_s"} as the max over ranks)."""
     import torch
 
-    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
-        return local % np.uint64(Q2)
-    t = torch.from_numpy(local.astype(np.int64))
-    if device is not None:
-        t = t.to(device)
-    dist.reduce(t, dst=dst, op=dist.ReduceOp.SUM)
-    if dist.get_rank() != dst:
-        return None
-    return (t.cpu().numpy().astype(np.uint64)) % np.uint64(Q2)
+    if dist is not None and dist.is_initialized():
+        dist.barrier()
+    t0 = time.perf_counter()
+    local = backend.encode(pv, payloads, first, total, rp, index_seed, weights)
+    backend.synchronize()
+    t1 = time.perf_counter()
+    red = reduce_digest(local, dist, dst)
+    backend.synchronize()
+    t2 = time.perf_counter()
+    times = [t1 - t0, t2 - t0]
+    if dist is not None and dist.is_initialized() and dist.get_world_size() > 1:
+        tt = torch.tensor(times, dtype=torch.float64, device=local.device)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        times = tt.tolist()
+    timing = {"encode_s": times[0], "encode_reduce_s": times[1]}
+    if red is None:
+        return None, timing
+    n = rp.max_encode_indices_cipher_count
+    return Digest(indices=red[:n], payloads=red[n:]), timing
 
 
 def run_omr_shard(backend, clue_a, clue_b, payloads, first: int, total: int, rp, index_seed: int,
-                  weights: np.ndarray, dist=None, device=None):
-    """Detect + encode this rank's shard and reduce the digest to rank 0.
+                  weights, dist=None):
+    """Detect + encode this rank's shard (global indices first..first+len) and reduce the digest
+    to rank 0. `rp` is the board-wide RetrievalParams (all_payloads_count == total); `weights`
+    the board-wide payload weights (omr_payload_weights). Returns (pv, Digest or None)."""
+    pv = backend.detect(clue_a, clue_b)
+    digest, _ = encode_and_reduce(backend, pv, payloads, first, total, rp, index_seed, weights, dist)
+    return pv, digest
 
-    clue_a/clue_b/payloads hold this rank's messages (global indices first..first+len).
-    `rp` is the board-wide RetrievalParams (all_payloads_count == total); `weights` the
-    board-wide payload weights (omr_payload_weights). Returns (pv, Digest or None)."""
-    pv = backend.detect_batch(clue_a, clue_b)
-    idx = np.stack([backend.encode_pertinent_indices(rp, pv, index_seed, ct, first)
-                    for ct in range(rp.max_encode_indices_cipher_count)])
-    pay = backend.encode_pertinent_payloads(pv, payloads, weights, rp, first)
-    local = np.concatenate([idx, pay]).astype(np.uint64)
-    red = reduce_digest(local, dist, device)
-    if red is None:
-        return pv, None
-    n = idx.shape[0]
-    return pv, Digest(indices=red[:n], payloads=red[n:])
+
+class GpuBackend:
+    """libomr_gpu.so on device buffers (torch tensors on `device`), enqueued on `stream`."""
+
+    def __init__(self, detector, device, stream):
+        self.det = detector
+        self.device = device
+        self.stream = stream
+        self._weights = None
+
+    def synchronize(self):
+        import torch
+        torch.cuda.synchronize(self.device)
+
+    def detect(self, clue_a, clue_b, out=None):
+        """clue_a int16 [D][512], clue_b int16 [D][7] device tensors -> pv int64 [D][2][2048]."""
+        import torch
+        D = clue_a.shape[0]
+        if out is None:
+            out = torch.empty((D, 2, 2048), dtype=torch.int64, device=self.device)
+        self.det.detect_batch_device(clue_a.data_ptr(), clue_b.data_ptr(), D, out.data_ptr(),
+                                     self.stream.cuda_stream)
+        return out
+
+    def encode(self, pv, payloads, first, total, rp, index_seed, weights):
+        import torch
+        n_idx, n_pay, per = rp.max_encode_indices_cipher_count, rp.cmb_cipher_count, rp.cmb_count_per_cipher
+        D = pv.shape[0]
+        if self._weights is None or self._weights[0] is not weights:
+            self._weights = (weights, torch.from_numpy(np.ascontiguousarray(weights).view(np.int16)).to(self.device))
+        d_w = self._weights[1]
+        d_pay = payloads if isinstance(payloads, torch.Tensor) else \
+            torch.from_numpy(np.ascontiguousarray(payloads, dtype=np.uint16).view(np.int16)).to(self.device)
+        dig = torch.empty((n_idx + n_pay, 2, 2048), dtype=torch.int64, device=self.device)
+        s = self.stream.cuda_stream
+        self.det.encode_indices_device(pv.data_ptr(), D, first, total, index_seed, 0, n_idx, dig.data_ptr(), s)
+        self.det.encode_payloads_device(pv.data_ptr(), d_pay.data_ptr(), D, first, total, d_w.data_ptr(), n_pay,
+                                        per, dig[n_idx:].data_ptr(), s)
+        return dig
