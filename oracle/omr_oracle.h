@@ -128,6 +128,24 @@ void oref_encode_payloads(const uint64_t *pv, const uint16_t *payloads, size_t D
  * retriever.rs:215-226; count draws into out. Returns number of rejected samples. */
 uint64_t oref_payload_weights(const uint8_t seed[32], size_t count, uint16_t *out);
 
+/* ---- key and clue generation (omr_oracle_keygen.c: key_gen/secret.rs:46-178,
+ *      key_gen/clue.rs:27-34; seeded ChaCha12 streams documented there) ---- */
+typedef struct {
+  uint8_t s0[OREF_N0];    /* clue LWE key, binary */
+  int8_t s1[OREF_N1];     /* first-level RLWE key, ternary */
+  uint8_t s_int[OREF_NI]; /* intermediate LWE key, binary */
+  int8_t s2[OREF_N2];     /* second-level RLWE key, ternary */
+  uint16_t pk_a[OREF_N0], pk_b[OREF_N0]; /* LwePublicKeyRlweMode (A, B = A s0 + E) */
+} oref_secret_pack;
+void oref_keygen_secret(uint64_t seed, oref_secret_pack *sk);
+/* Keys in the layout of oref_create; OpenMP over key rows with nthreads threads. */
+void oref_keygen_detection_key(const oref_secret_pack *sk, uint64_t seed, uint32_t *bsk1, uint32_t *ksk,
+                               uint64_t *bsk2, uint64_t *tk, int nthreads);
+/* Clues for global message indices [first, first + count): clue_a u16 [count][512],
+ * clue_b u16 [count][7]. */
+void oref_gen_clues(const oref_secret_pack *sk, uint64_t seed, uint64_t first, size_t count,
+                    uint16_t *clue_a, uint16_t *clue_b, int nthreads);
+
 /* ---- client-side helpers for KATs (retriever.rs, omd.rs) ---- */
 /* s2: ternary secret (int8, 2048). ct: NTT-domain (a,b). out: coefficient-domain phase. */
 void oref_decrypt_ntt(const int8_t *s2, const uint64_t *ct, uint64_t *out);

@@ -58,6 +58,9 @@ def lib():
         "oref_decrypt_ntt": (None, [_i8p, _u64p, _u64p]),
         "oref_decode_coeff": (C.c_uint32, [C.c_uint64]),
         "oref_clue_phase": (C.c_uint32, [_u16p, _u16p, C.c_int, _u8p]),
+        "oref_keygen_secret": (None, [C.c_uint64, C.c_void_p]),
+        "oref_keygen_detection_key": (None, [C.c_void_p, C.c_uint64, _u32p, _u32p, _u64p, _u64p, C.c_int]),
+        "oref_gen_clues": (None, [C.c_void_p, C.c_uint64, C.c_uint64, C.c_size_t, _u16p, _u16p, C.c_int]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -118,6 +121,38 @@ class OracleDetector:
         lib().oref_detect_batch(self._h, np.ascontiguousarray(clue_a, dtype=np.uint16).reshape(-1),
                                 np.ascontiguousarray(clue_b, dtype=np.uint16).reshape(-1), D, out, int(nthreads))
         return out.reshape(D, 2, 2048)
+
+
+class SecretPack(C.Structure):
+    """oref_secret_pack (key_gen/secret.rs:46-107 restated in oracle/omr_oracle_keygen.c)."""
+    _fields_ = [("s0", C.c_uint8 * 512), ("s1", C.c_int8 * 1024), ("s_int", C.c_uint8 * 670),
+                ("s2", C.c_int8 * 2048), ("pk_a", C.c_uint16 * 512), ("pk_b", C.c_uint16 * 512)]
+
+    @classmethod
+    def generate(cls, seed: int) -> "SecretPack":
+        sk = cls()
+        lib().oref_keygen_secret(seed, C.byref(sk))
+        return sk
+
+    def export(self):
+        return dict(s0=np.ctypeslib.as_array(self.s0).copy(), s1=np.ctypeslib.as_array(self.s1).copy(),
+                    s_int=np.ctypeslib.as_array(self.s_int).copy(), s2=np.ctypeslib.as_array(self.s2).copy())
+
+    def generate_detection_key(self, seed: int, nthreads: int = 8):
+        """(bsk1, ksk, bsk2, trace_key) in the include/omr_gpu.h layout."""
+        bsk1 = np.empty((512, 8, 2, 1024), np.uint32)
+        ksk = np.empty((1024, 27, 671), np.uint32)
+        bsk2 = np.empty((670, 12, 2, 2048), np.uint64)
+        tk = np.empty((11, 25, 2, 2048), np.uint64)
+        lib().oref_keygen_detection_key(C.byref(self), seed, bsk1.reshape(-1), ksk.reshape(-1), bsk2.reshape(-1),
+                                        tk.reshape(-1), nthreads)
+        return bsk1, ksk, bsk2, tk
+
+    def gen_clues(self, seed: int, first: int, count: int, nthreads: int = 8):
+        a = np.empty((count, 512), np.uint16)
+        b = np.empty((count, 7), np.uint16)
+        lib().oref_gen_clues(C.byref(self), seed, first, count, a.reshape(-1), b.reshape(-1), nthreads)
+        return a, b
 
 
 def ntt(level, a):

@@ -204,32 +204,39 @@ def _host(t, dtype):
     return t.cpu().numpy().view(dtype)
 
 
-def test_gpu_clue_generation_matches_host():
-    """omr_gen_clues_device == the host generator, bit for bit, for both packs,
-    at an offset global index (stream id = global message index)."""
+def test_gpu_clue_generation_matches_oracle():
+    """omr_gen_clues_device (SURVEY.md §8 f1) == the oracle's ClueKey::gen_clues restatement
+    (oracle/omr_oracle_keygen.c, clue.rs:27-34) and the host generator, bit for bit, for both
+    packs, at an offset global index (stream id = global message index)."""
     a_sk, b_sk, _ = PL.keys()
-    for sk, seed, first, count in ((a_sk, 1000, 0, 257), (b_sk, 1001, 123456, 1000)):
-        ha, hb = sk.gen_clues(seed, first, count)
+    for sk, pseed, seed, first, count in ((a_sk, PL.SK_SEED, 1000, 0, 257), (b_sk, PL.SK2_SEED, 1001, 123456, 1000)):
+        oa, ob = O.SecretPack.generate(pseed).gen_clues(seed, first, count)
         da, db = _dev_u(count * A.N0, 2), _dev_u(count * A.CLUE_COUNT, 2)
         sk.gen_clues_device(seed, first, count, da.data_ptr(), db.data_ptr())
-        assert np.array_equal(_host(da, np.uint16).reshape(ha.shape), ha)
-        assert np.array_equal(_host(db, np.uint16).reshape(hb.shape), hb)
+        assert np.array_equal(_host(da, np.uint16).reshape(oa.shape), oa)
+        assert np.array_equal(_host(db, np.uint16).reshape(ob.shape), ob)
+        ha, hb = sk.gen_clues(seed, first, count)
+        assert np.array_equal(ha, oa) and np.array_equal(hb, ob)
 
 
-def test_gpu_keygen_matches_host_and_detects():
-    """omr_keygen_detection_key_device == the host key generator, bit for bit
-    (all four components, including rejection-sampled rows), and a Detector built straight
-    from the device-resident key gives the same detect output as one built from host keys."""
-    a_sk, b_sk, dk = PL.keys()
+def test_gpu_keygen_matches_oracle_and_detects():
+    """omr_keygen_detection_key_device == the oracle's generate_detection_key
+    restatement (oracle/omr_oracle_keygen.c, secret.rs:118-178), bit for bit (all four
+    components, including rejection-sampled rows), and a Detector built straight from the
+    device-resident key gives the same detect output as the oracle."""
+    a_sk, _, dk = PL.keys()
+    ref = O.SecretPack.generate(PL.SK_SEED).generate_detection_key(PL.KEY_SEED, nthreads=16)
     parts = [(dk.bsk1, 4), (dk.ksk, 4), (dk.bsk2, 8), (dk.trace_key, 8)]
     bufs = [_dev_u(h.size, it) for h, it in parts]
     a_sk.generate_detection_key_device(PL.KEY_SEED, *[b.data_ptr() for b in bufs])
-    for (h, _), b in zip(parts, bufs):
-        assert np.array_equal(_host(b, h.dtype).reshape(h.shape), h)
+    for (h, _), b, r in zip(parts, bufs, ref):
+        assert np.array_equal(_host(b, h.dtype).reshape(h.shape), r)
     mask = np.zeros(6, bool)
     mask[[1, 4]] = True
     ca, cb = PL.mixed_clues(mask, seed=77)
-    want = A.Detector(dk).detect_batch(ca, cb)
+    orc = O.OracleDetector(*ref)
+    want = orc.detect_batch(ca, cb, nthreads=6)
+    orc.close()
     det = A.Detector.from_device_key(*[b.data_ptr() for b in bufs])
     del bufs  # the context holds its own converted copy
     assert np.array_equal(det.detect_batch(ca, cb), want)

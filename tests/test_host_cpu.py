@@ -107,3 +107,22 @@ def test_on_disk_formats_round_trip(tmp_path):
     (tmp_path / "x.bin").write_bytes(b"not a container")
     with pytest.raises(A.OmrError):
         A.load_ciphertexts(str(tmp_path / "x.bin"))
+
+
+def test_host_keygen_and_clues_match_oracle():
+    """The product's host generators (keygen.hip) == the oracle's restatement of
+    SecretKeyPack::new / generate_detection_key / ClueKey::gen_clues (oracle/omr_oracle_keygen.c),
+    bit for bit, on the same seeded streams: secret keys, every component of the detection key,
+    and clues at an offset global index."""
+    a, b, dk = PL.keys()
+    for pack, seed in ((a, PL.SK_SEED), (b, PL.SK2_SEED)):
+        osk = O.SecretPack.generate(seed)
+        mine, ref = pack.export(), osk.export()
+        for k in ("s0", "s1", "s_int", "s2"):
+            assert np.array_equal(mine[k], ref[k]), k
+        ha, hb = pack.gen_clues(1000 + seed, 123456, 37)
+        oa, ob = osk.gen_clues(1000 + seed, 123456, 37)
+        assert np.array_equal(ha, oa) and np.array_equal(hb, ob)
+    ref = O.SecretPack.generate(PL.SK_SEED).generate_detection_key(PL.KEY_SEED, nthreads=8)
+    for name, x, y in zip(("bsk1", "ksk", "bsk2", "trace_key"), (dk.bsk1, dk.ksk, dk.bsk2, dk.trace_key), ref):
+        assert np.array_equal(x, y), name

@@ -1,0 +1,83 @@
+"""The Rust FFI crate (rust/omr-gpu-sys) against the C header it binds (include/omr_gpu.h).
+
+cargo/rustc are absent from this image, so the crate cannot be built here; this check stands in
+for the build: every function the header declares has exactly one `extern "C"` declaration in
+src/lib.rs with the same name, the same number of parameters and the same pointer / value shape
+per parameter, and the crate declares nothing the header does not. The #[repr(C)] structs carry
+the header's fields in order."""
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HDR = os.path.join(ROOT, "include", "omr_gpu.h")
+LIB = os.path.join(ROOT, "rust", "omr-gpu-sys", "src", "lib.rs")
+
+
+def _split_params(s):
+    s = s.strip()
+    if s in ("", "void"):
+        return []
+    return [p.strip() for p in s.split(",")]
+
+
+def header_functions():
+    text = re.sub(r"/\*.*?\*/", " ", open(HDR).read(), flags=re.S)
+    out = {}
+    for m in re.finditer(r"\b[\w\s\*]+?\b(omr_[a-z0-9_]+)\s*\(([^;{]*?)\)\s*;", text):
+        params = _split_params(m.group(2))
+        out[m.group(1)] = ["ptr" if "*" in p or "[" in p else "val" for p in params]
+    return out
+
+
+def rust_functions():
+    text = open(LIB).read()
+    block = text[text.index('extern "C" {'):]
+    block = block[:block.index("\n    }\n")]
+    block = re.sub(r"//[^\n]*", " ", block)
+    out = {}
+    for m in re.finditer(r"pub fn (omr_[a-z0-9_]+)\s*\((.*?)\)\s*(->\s*[^;]+)?;", block, flags=re.S):
+        assert m.group(1) not in out, f"duplicate declaration {m.group(1)}"
+        params = _split_params(m.group(2))
+        out[m.group(1)] = ["ptr" if "*mut" in p or "*const" in p else "val" for p in params]
+    return out
+
+
+def test_every_header_function_bound_with_same_shape():
+    h, r = header_functions(), rust_functions()
+    assert len(h) >= 30, sorted(h)
+    assert set(h) == set(r), f"header only {sorted(set(h) - set(r))}, crate only {sorted(set(r) - set(h))}"
+    for name in sorted(h):
+        assert h[name] == r[name], f"{name}: header {h[name]} vs crate {r[name]}"
+
+
+@pytest.mark.parametrize("c_name,rust_name", [("omr_retrieval_params", "OmrRetrievalParams"),
+                                              ("omr_detection_key_view", "OmrDetectionKeyView"),
+                                              ("omr_detect_timing", "OmrDetectTiming")])
+def test_repr_c_structs_match_header(c_name, rust_name):
+    text = re.sub(r"/\*.*?\*/", " ", open(HDR).read(), flags=re.S)
+    body = re.search(r"typedef struct \{([^{}]*)\}\s*" + c_name + ";", text).group(1)
+    c_fields = []
+    for decl in body.split(";"):
+        decl = decl.strip()
+        if not decl:
+            continue
+        names = decl.split(None, 1)[1] if not decl.startswith("const") else decl.split(None, 2)[2]
+        c_fields += [n.strip().lstrip("*").strip() for n in names.split(",")]
+    rs = open(LIB).read()
+    rbody = re.search(r"pub struct " + rust_name + r" \{(.*?)\}", rs, flags=re.S).group(1)
+    r_fields = re.findall(r"pub (\w+):", rbody)
+    assert c_fields == r_fields
+
+
+def test_crate_layout_and_link_directives():
+    crate = os.path.join(ROOT, "rust", "omr-gpu-sys")
+    toml = open(os.path.join(crate, "Cargo.toml")).read()
+    assert 'links = "omr_gpu"' in toml and 'name = "omr-gpu-sys"' in toml
+    build = open(os.path.join(crate, "build.rs")).read()
+    assert "rustc-link-lib=dylib=omr_gpu" in build
+    lib = open(LIB).read()
+    for api in ("pub fn detect(", "pub fn detect_batch(", "pub fn encode_pertinent_indices(",
+                "pub fn encode_pertinent_payloads(", "pub fn detect_with_time_info(", "pub fn decode_digest("):
+        assert api in lib, api
