@@ -308,17 +308,26 @@ def main():
                    "digest_bytes": int((rp.max_encode_indices_cipher_count + rp.cmb_cipher_count) * 2 * 2048 * 8),
                    "collective": "reduce(sum) over RCCL" if dist else "none", "pertinent_recovered": len(indices)}
 
-    latency_ms = None
+    latency_ms = latency_tp_ms = None
     if not args.no_latency:
+        # one message end to end (detect on device buffers, wall clock): the latency kernels
+        # (default for chunks up to 64 messages) and, for comparison, the throughput kernels
         one_out = torch.empty((1, 2, 2048), dtype=torch.int64, device=dev)
-        lat = []
-        for _ in range(3):
-            torch.cuda.synchronize(dev)
-            t1 = time.perf_counter()
-            det.detect_batch_device(d_ca.data_ptr(), d_cb.data_ptr(), 1, one_out.data_ptr(), stream.cuda_stream)
-            torch.cuda.synchronize(dev)
-            lat.append((time.perf_counter() - t1) * 1e3)
-        latency_ms = round(min(lat), 3)
+
+        def one_message():
+            lat = []
+            for _ in range(3):
+                torch.cuda.synchronize(dev)
+                t1 = time.perf_counter()
+                det.detect_batch_device(d_ca.data_ptr(), d_cb.data_ptr(), 1, one_out.data_ptr(), stream.cuda_stream)
+                torch.cuda.synchronize(dev)
+                lat.append((time.perf_counter() - t1) * 1e3)
+            return round(min(lat), 3)
+
+        latency_ms = one_message()
+        det.set_latency_threshold(0)
+        latency_tp_ms = one_message()
+        det.set_latency_threshold(64)
 
     if rank != 0:
         if dist:
@@ -351,6 +360,7 @@ def main():
                    "messages_per_gpu": D, "messages_total": total,
                    "pertinent": int(len(pert)), "batch": args.batch, "parallelism": f"dp{world}"},
         "latency_ms_per_message": latency_ms,
+        "latency_ms_per_message_throughput_kernels": latency_tp_ms,
         "stage_ms_per_step": {k: round(v / args.steps, 2) for k, v in stage.items()},
         "detect_bytes_per_message": DETECT_BYTES,
         "roofline": roof,

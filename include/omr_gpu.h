@@ -156,6 +156,10 @@ const char *omr_detect_kernels(void);
 /* Messages per internal detect chunk (memory/latency knob: 36 KiB of scratch per message);
  * 0 = the default 16,384. */
 omr_status omr_ctx_set_batch(omr_ctx *ctx, size_t batch);
+/* Chunks of at most `max_messages` messages run the latency kernels (each level-1 rotation and
+ * each level-2 message spread over more waves: lower single-message latency, bit-identical
+ * output); larger chunks run the throughput kernels. Default 64; 0 = always throughput. */
+omr_status omr_ctx_set_latency_threshold(omr_ctx *ctx, size_t max_messages);
 
 /* Detector::detect (detector.rs:135-166), batched like `par_iter().map(detect)` in
  * examples/omr.rs:160-164. Host buffers: clue_a u16 [D][512], clue_b u16 [D][7],

@@ -76,16 +76,23 @@ def structured():
     det.close()
 
 
-def test_structured_stages(structured):
+@pytest.mark.parametrize("threshold", [64, 0])
+def test_structured_stages(structured, threshold):
+    """Every stage on structured keys against the independent model's golden vectors, through the
+    latency kernels (threshold 64) and the throughput kernels (threshold 0)."""
     det, e = structured
-    la = np.zeros(512, dtype=np.uint16)
-    lb = np.zeros(1, dtype=np.uint16)
-    O.lib().oref_extract_clue(e["clue_a"], e["clue_b"], 0, la, lb)
-    assert np.array_equal(det.blind_rotate_level1(la, lb)[0], e["br1_clue0"])
-    assert np.array_equal(det.first_level(e["clue_a"], e["clue_b"])[0], e["lwe_int"])
-    assert np.array_equal(det.blind_rotate_level2(e["lwe_int"])[0], e["br2"])
-    assert np.array_equal(det.second_level(e["lwe_int"])[0], e["detect"])
-    assert np.array_equal(det.detect(e["clue_a"], e["clue_b"]), e["detect"])
+    det.set_latency_threshold(threshold)
+    try:
+        la = np.zeros(512, dtype=np.uint16)
+        lb = np.zeros(1, dtype=np.uint16)
+        O.lib().oref_extract_clue(e["clue_a"], e["clue_b"], 0, la, lb)
+        assert np.array_equal(det.blind_rotate_level1(la, lb)[0], e["br1_clue0"])
+        assert np.array_equal(det.first_level(e["clue_a"], e["clue_b"])[0], e["lwe_int"])
+        assert np.array_equal(det.blind_rotate_level2(e["lwe_int"])[0], e["br2"])
+        assert np.array_equal(det.second_level(e["lwe_int"])[0], e["detect"])
+        assert np.array_equal(det.detect(e["clue_a"], e["clue_b"]), e["detect"])
+    finally:
+        det.set_latency_threshold(64)
 
 
 @pytest.fixture(scope="module")
@@ -98,7 +105,17 @@ def real():
     orc.close()
 
 
-def test_real_keys_detect_bit_exact_and_kat(real):
+@pytest.fixture(params=["latency", "throughput"])
+def path(request, real):
+    """Both kernel families on the same small inputs: the latency kernels (chunks up to 64
+    messages by default, latency_kernels.hpp) and the throughput kernels (threshold 0)."""
+    det = real[1]
+    det.set_latency_threshold(64 if request.param == "latency" else 0)
+    yield request.param
+    det.set_latency_threshold(64)
+
+
+def test_real_keys_detect_bit_exact_and_kat(real, path):
     a, det, orc = real
     s2 = a.export()["s2"]
     mask = np.array([1, 0, 1, 0, 0, 1, 0, 1], dtype=bool)
@@ -114,7 +131,7 @@ def test_real_keys_detect_bit_exact_and_kat(real):
             assert not dec.any()
 
 
-def test_real_keys_stage_parity(real):
+def test_real_keys_stage_parity(real, path):
     _, det, orc = real
     ca, cb = PL.mixed_clues([True, False, False], seed=7)
     fl = det.first_level(ca, cb)
@@ -242,7 +259,20 @@ def test_gpu_keygen_matches_oracle_and_detects():
     assert np.array_equal(det.detect_batch(ca, cb), want)
 
 
-def test_edge_inputs_bit_exact(real):
+def test_level1_rotations_both_paths(real, path):
+    """omr_blind_rotate_level1 (full RLWE output) on explicit LWEs, incl. a = 0 steps and the
+    extreme phases, bit-exact against the oracle's blind rotation."""
+    _, det, orc = real
+    rng = np.random.default_rng(17)
+    la = rng.integers(0, 2048, (5, A.N0)).astype(np.uint16)
+    la[1, ::3] = 0
+    lb = np.array([0, 1, 1023, 1024, 2047], np.uint16)
+    got = det.blind_rotate_level1(la, lb)
+    for m in range(5):
+        assert np.array_equal(got[m], orc.br1(la[m], lb[m])), f"rotation {m}"
+
+
+def test_edge_inputs_bit_exact(real, path):
     """Inputs the KATs never produce, bit-exact against the oracle: all-zero clues (every CMUX
     step has a_i = 0), all-maximal clues (a_i = 2047), uniformly random clue words (not
     encryptions), and a ragged batch split into chunks of 5 (12 = 5 + 5 + 2, and 7 rotations per

@@ -15,6 +15,7 @@
 
 #include "detect_kernels.hpp"
 #include "encode_kernels.hpp"
+#include "latency_kernels.hpp"
 
 using namespace omr;
 
@@ -99,6 +100,10 @@ std::vector<double2> fft_twiddles(int T, int E, int L) {
 
 }  // namespace
 
+#ifndef OMR_DEFAULT_LATENCY_MAX
+#define OMR_DEFAULT_LATENCY_MAX 64  // chunks up to this many messages run the latency kernels
+#endif
+
 struct omr_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -111,6 +116,9 @@ struct omr_ctx {
   DeviceTables tb{};
   size_t batch = OMR_DEFAULT_BATCH, batch_cap = 0;
   uint32_t *ext = nullptr, *lwe1t = nullptr, *lwe_int = nullptr;
+  // chunks of at most latency_max messages run the latency kernels (latency_kernels.hpp)
+  size_t latency_max = OMR_DEFAULT_LATENCY_MAX;
+  int *ks_part = nullptr;  // split key-switch partial sums, [KS_SPLIT][64][672][4]
   // host-API staging
   uint16_t *s_clue_a = nullptr, *s_clue_b = nullptr;
   uint64_t *s_out = nullptr;
@@ -174,6 +182,7 @@ omr_status ensure_batch(omr_ctx *c, size_t B) {
   HIP_TRY(hipMalloc(&c->ext, B * CLUES * (N1 + 1) * sizeof(uint32_t)));
   HIP_TRY(hipMalloc(&c->lwe1t, B * (N1 + 1) * sizeof(uint32_t)));
   HIP_TRY(hipMalloc(&c->lwe_int, B * (NI + 1) * sizeof(uint32_t)));
+  if (!c->ks_part) HIP_TRY(hipMalloc(&c->ks_part, (size_t)KS_SPLIT * 64 * KSM_COLS * KSM_LIMBS * sizeof(int)));
   c->batch_cap = B;
   return OMR_OK;
 }
@@ -224,20 +233,33 @@ omr_status convert_keys_fft1(const uint32_t *host, size_t npoly, double2 *dev, c
   return OMR_OK;
 }
 
-// LWE key switch + modulus switch of B messages (lwe1t [1025][B] -> out [B][671]).
+bool latency_path(const omr_ctx *c, size_t n) { return n <= c->latency_max; }
+
+// LWE key switch + modulus switch of B messages (lwe1t [1025][B] -> out [B][671]). Up to 64
+// messages (the latency path) the input coefficients are split over KS_SPLIT workgroup slices.
 omr_status launch_ks(omr_ctx *c, int B, uint32_t *out, hipStream_t st) {
-  ks_mfma_kernel<<<dim3((B + 63) / 64, KSM_COLS / 32), 64, 0, st>>>(c->lwe1t, c->kskb, out, B);
+  if (latency_path(c, (size_t)B) && B <= 64) {
+    ks_mfma_split_kernel<<<dim3(1, KSM_COLS / 32, KS_SPLIT), 64, 0, st>>>(c->lwe1t, c->kskb, c->ks_part, B, 64);
+    HIP_TRY(hipGetLastError());
+    ks_combine_kernel<<<(B * (NI + 1) + 255) / 256, 256, 0, st>>>(c->ks_part, c->lwe1t, out, B, 64);
+  } else {
+    ks_mfma_kernel<<<dim3((B + 63) / 64, KSM_COLS / 32), 64, 0, st>>>(c->lwe1t, c->kskb, out, B);
+  }
   HIP_TRY(hipGetLastError());
   return OMR_OK;
 }
 
 // Level-1 blind rotations of n (message, clue) pairs (mode 0: clue g % 7 of message g / 7 ->
 // extracted LWE; mode 1: explicit LWEs -> full RLWE), BR1F_WPG rotations per workgroup.
+// `msgs`: the messages of the chunk (selects the latency kernels, one workgroup per rotation).
 omr_status launch_br1(omr_ctx *c, size_t n, const uint16_t *ca, const uint16_t *cb,
                       const uint16_t *la, const uint16_t *lb, uint32_t *ext, uint64_t *rlwe, int mode,
-                      hipStream_t st) {
-  br1f_kernel<<<(unsigned)((n + BR1F_WPG - 1) / BR1F_WPG), 64 * BR1F_WPG, 0, st>>>(
-      ca, cb, la, lb, c->bsk1f, c->tb, ext, rlwe, mode, n);
+                      hipStream_t st, size_t msgs) {
+  if (latency_path(c, msgs))
+    br1l_kernel<<<(unsigned)n, 64 * BR1L_WAVES, 0, st>>>(ca, cb, la, lb, c->bsk1f, c->tb, ext, rlwe, mode);
+  else
+    br1f_kernel<<<(unsigned)((n + BR1F_WPG - 1) / BR1F_WPG), 64 * BR1F_WPG, 0, st>>>(
+        ca, cb, la, lb, c->bsk1f, c->tb, ext, rlwe, mode, n);
   HIP_TRY(hipGetLastError());
   return OMR_OK;
 }
@@ -245,7 +267,15 @@ omr_status launch_br1(omr_ctx *c, size_t n, const uint16_t *ca, const uint16_t *
 // Level-2 blind rotation (+ trace, mode 0) of n LWE(670, 4096) ciphertexts, one workgroup each.
 omr_status launch_br2(omr_ctx *c, size_t n, const uint32_t *lwe_int, uint64_t *out, int mode,
                       hipStream_t st) {
-  br2_trace_kernel<<<(unsigned)n, BR2_T, 0, st>>>(lwe_int, c->bsk2, c->tk, c->tb, out, mode);
+  if (latency_path(c, n)) {  // two 4-wave groups per message, then the trace in place
+    br2l_kernel<<<(unsigned)n, BR2L_T, 0, st>>>(lwe_int, c->bsk2, c->tb, out);
+    if (mode == 0) {
+      HIP_TRY(hipGetLastError());
+      trace_kernel<<<(unsigned)n, BR2_T, 0, st>>>(out, c->tk, c->tb);
+    }
+  } else {
+    br2_trace_kernel<<<(unsigned)n, BR2_T, 0, st>>>(lwe_int, c->bsk2, c->tk, c->tb, out, mode);
+  }
   HIP_TRY(hipGetLastError());
   return OMR_OK;
 }
@@ -374,6 +404,7 @@ extern "C" void omr_ctx_destroy(omr_ctx *c) {
   dev_free(c->s_clue_b);
   dev_free(c->s_out);
   dev_free(c->partial);
+  dev_free(c->ks_part);
   for (auto e : c->events) (void)hipEventDestroy(e);
   if (c->scratch_free) (void)hipEventDestroy(c->scratch_free);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -391,6 +422,13 @@ extern "C" omr_status omr_ctx_set_batch(omr_ctx *c, size_t batch) {
   c->batch = batch ? batch : OMR_DEFAULT_BATCH;
   HIP_TRY(hipSetDevice(c->device));
   return ensure_batch(c, c->batch);
+}
+
+extern "C" omr_status omr_ctx_set_latency_threshold(omr_ctx *c, size_t max_messages) {
+  if (!c) return set_error(OMR_ERR_INVALID_ARGUMENT, "omr_ctx_set_latency_threshold: NULL ctx");
+  std::lock_guard<std::mutex> lk(c->mu);
+  c->latency_max = max_messages;
+  return OMR_OK;
 }
 
 extern "C" omr_status omr_ctx_enable_timing(omr_ctx *c, int enable) {
@@ -425,7 +463,7 @@ omr_status detect_device(omr_ctx *c, const uint16_t *ca, const uint16_t *cb, siz
     hipEvent_t *ev = c->timing ? &c->events[ch * 4] : nullptr;
     if (ev) HIP_TRY(hipEventRecord(ev[0], st));
     if ((s = launch_br1(c, (size_t)B * CLUES, ca + off * N0, cb + off * CLUES, nullptr, nullptr,
-                        c->ext, nullptr, 0, st)) != OMR_OK)
+                        c->ext, nullptr, 0, st, (size_t)B)) != OMR_OK)
       return s;
     if (ev) HIP_TRY(hipEventRecord(ev[1], st));
     const size_t n7 = (size_t)B * (N1 + 1);
@@ -675,7 +713,7 @@ extern "C" omr_status omr_first_level(omr_ctx *c, const uint16_t *ca, const uint
   HIP_TRY(hipMemcpyAsync(c->s_clue_b, cb, D * CLUES * sizeof(uint16_t), hipMemcpyHostToDevice, st));
   const int B = (int)D;
   if ((s = launch_br1(c, (size_t)B * CLUES, c->s_clue_a, c->s_clue_b, nullptr, nullptr, c->ext,
-                      nullptr, 0, st)) != OMR_OK)
+                      nullptr, 0, st, (size_t)B)) != OMR_OK)
     return s;
   const size_t n7 = (size_t)B * (N1 + 1);
   sum7_kernel<<<(unsigned)((n7 + 255) / 256), 256, 0, st>>>(c->ext, c->lwe1t, B);
@@ -723,7 +761,7 @@ extern "C" omr_status omr_blind_rotate_level1(omr_ctx *c, const uint16_t *la, co
   HIP_TRY(dout.alloc(n * 2 * N1));
   HIP_TRY(hipMemcpy(da.p, la, n * N0 * sizeof(uint16_t), hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(db.p, lb, n * sizeof(uint16_t), hipMemcpyHostToDevice));
-  omr_status s = launch_br1(c, n, nullptr, nullptr, da.p, db.p, nullptr, dout.p, 1, c->stream);
+  omr_status s = launch_br1(c, n, nullptr, nullptr, da.p, db.p, nullptr, dout.p, 1, c->stream, n);
   if (s != OMR_OK) return s;
   HIP_TRY(hipStreamSynchronize(c->stream));
   HIP_TRY(hipMemcpy(out, dout.p, n * 2 * N1 * sizeof(uint64_t), hipMemcpyDeviceToHost));

@@ -1,5 +1,5 @@
-// LWE key switch on the matrix cores (OMR_KS_MFMA; NonPowOf2LweKeySwitchingKey::key_switch,
-// detector.rs:560-563, with the modulus switch :571-575 and offset :577-594 as in ks_kernel).
+// LWE key switch on the matrix cores (NonPowOf2LweKeySwitchingKey::key_switch, detector.rs:560-563,
+// with the modulus switch :571-575 and offset :577-594).
 //
 // The key switch is a binary-by-integer matrix product:
 //   acc[m][col] = sum_i sum_j bit_j(x[m][i]) * KSK[i][j][col]      (i < 1024, j < 27, col <= 670)
@@ -7,7 +7,7 @@
 // B_l[32 i + j][col] = the l-th 7-bit limb of KSK[i][j][col] (l = 0..3, 28 bits >= 27), one
 // v_mfma_i32_32x32x32_i8 per (32 messages x 32 columns x 32 digits x limb). Per limb the int32
 // sums stay below 27648 * 127 < 2^22; acc = sum_l C_l 2^(7 l) < 2^43 is exact in int64 and then
-// reduced mod q1 like ks_kernel's u64 sum, so the output is bit-identical.
+// reduced mod q1 like the oracle's u64 sum, so the output is bit-identical.
 #pragma once
 
 #include "kernels.hpp"
@@ -40,6 +40,17 @@ __global__ void ksk_to_i8_kernel(const uint32_t *__restrict__ ksk, uint32_t *__r
     word |= v << (8 * b);
   }
   out[t] = word;
+}
+
+// Output column `col` of one message from the exact key-switch sum (detector.rs:560-594):
+// b' = b - sum (columns < 670: -sum), modulus switch q1 -> 4096 (round half up), and the
+// offset b += 7 * 128 on the body.
+__device__ __forceinline__ uint32_t ks_epilogue(uint64_t sum, uint64_t bq, int col) {
+  const uint64_t s = sum % Q1;
+  uint64_t v = col < NI ? (Q1 - s) % Q1 : (bq + Q1 - s) % Q1;
+  v = ((2ull * QI * v + Q1) / (2ull * Q1)) % QI;
+  if (col == NI) v = (v + CLUES * (QI / TI)) % QI;
+  return (uint32_t)v;
 }
 
 // 0/1 bytes of the 16 bits of x starting at bit `base` (A fragment: 16 int8 per lane): each
@@ -90,12 +101,7 @@ __global__ __launch_bounds__(64, 2) void ks_mfma_kernel(const uint32_t *__restri
       if (m >= B) continue;
       const uint64_t sum = (uint64_t)acc[t][0][reg] + ((uint64_t)acc[t][1][reg] << 7) +
                            ((uint64_t)acc[t][2][reg] << 14) + ((uint64_t)acc[t][3][reg] << 21);
-      const uint64_t s = sum % Q1;
-      const uint64_t bq = lwe1t[(size_t)N1 * B + m];
-      uint64_t v = col < NI ? (Q1 - s) % Q1 : (bq + Q1 - s) % Q1;
-      v = ((2ull * QI * v + Q1) / (2ull * Q1)) % QI;
-      if (col == NI) v = (v + CLUES * (QI / TI)) % QI;
-      lwe_int[(size_t)m * (NI + 1) + col] = (uint32_t)v;
+      lwe_int[(size_t)m * (NI + 1) + col] = ks_epilogue(sum, lwe1t[(size_t)N1 * B + m], col);
     }
 }
 

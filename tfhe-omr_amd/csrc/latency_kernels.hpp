@@ -1,0 +1,354 @@
+// Latency path of the detect pipeline (small chunks: a single message or a few).
+//
+// The throughput kernels give one wave to a level-1 rotation and one 4-wave workgroup to a
+// level-2 message, so a lone message walks 512 (670) CMUX steps with 10 (14) transforms each on
+// one wave (workgroup) while the rest of the chip idles: 9 + 16.6 ms of its 27 ms latency.
+// Here every CMUX step's digit transforms are split over more waves, whose partial
+// multiply-accumulates are summed through LDS before the inverse transforms:
+//   level 1 (br1l_kernel): one 4-wave workgroup per rotation; wave w transforms mask digit w and
+//     body digit w (2 FFTs instead of 8), waves 0 / 1 sum the partials of output A / B, run its
+//     inverse FFT and own the mask / body accumulator;
+//   level 2 (br2l_kernel): one 8-wave workgroup per message, two groups of four waves; group 0
+//     transforms the 6 mask digits, group 1 the 6 body digits, each sums one output and runs one
+//     inverse NTT (6 + 1 transforms per group instead of 12 + 2); the trace runs after it
+//     (trace_kernel, in place on the output);
+//   key switch (ks_mfma_split_kernel + ks_combine_kernel): the 1024 input coefficients split
+//     over 32 slices of workgroups (a lone message otherwise gets 21 waves for 88 MB of KSK).
+// The arithmetic is the throughput kernels' (same digits, transforms, products and reduction
+// points), so the outputs are bit-identical; tests/test_gpu_parity.py checks both paths.
+#pragma once
+
+#include "detect_kernels.hpp"
+
+namespace omr {
+
+// ---- level 1 ---------------------------------------------------------------------------------
+constexpr int BR1L_WAVES = D1;  // one wave per gadget digit (mask and body digit w)
+
+__global__ __launch_bounds__(64 * BR1L_WAVES, 1) void br1l_kernel(
+    const uint16_t *__restrict__ clue_a, const uint16_t *__restrict__ clue_b,
+    const uint16_t *__restrict__ lwe_a, const uint16_t *__restrict__ lwe_b,
+    const double2 *__restrict__ bskf, DeviceTables tb, uint32_t *__restrict__ ext_out,
+    uint64_t *__restrict__ rlwe_out, int mode) {
+  using F = Fft512;
+  constexpr int NF = F::N, W = BR1L_WAVES;
+  __shared__ int ext[2][2 * N1];               // [ACC, -ACC] per poly (0 mask, 1 body)
+  __shared__ double2 xch_all[W][2 * F::BUF];   // per wave: two interleaved transforms
+  __shared__ double2 part[W][2][8 * 64];       // partial outputs A, B: slot e * 64 + lane
+  __shared__ double2 tws[NF];
+  __shared__ uint16_t la[N0];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  double2 *xch = xch_all[wave];
+  const size_t g = blockIdx.x;  // rotation
+  int b;
+  if (lwe_a == nullptr) {  // clue g % 7 of message g / 7 (CmLweCiphertext::extract_all, :514)
+    const size_t m = g / CLUES;
+    const int c = (int)(g % CLUES);
+    const uint16_t *A = clue_a + m * N0;
+    for (int i = threadIdx.x; i < N0; i += 64 * W)
+      la[i] = i <= c ? (uint16_t)(A[c - i] & (Q0 - 1)) : (uint16_t)((Q0 - A[N0 + c - i]) & (Q0 - 1));
+    b = clue_b[m * CLUES + c] & (Q0 - 1);
+  } else {
+    for (int i = threadIdx.x; i < N0; i += 64 * W) la[i] = lwe_a[g * N0 + i] & (Q0 - 1);
+    b = lwe_b[g] & (Q0 - 1);
+  }
+  // ACC = (0, X^{-b} * LUT1): wave 0 owns the mask accumulator, wave 1 the body accumulator
+  int ac[16];
+  const int r0 = (2 * N1 - (b % (2 * N1))) % (2 * N1);
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+    ac[i] = wave == 1 ? (int)canon_small<Mod<1>>(rot_read<N1>(tb.lut1, acc_coef(lane, i), r0)) : 0;
+  if (wave < 2) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      ext[wave][acc_coef(lane, i)] = ac[i];
+      ext[wave][N1 + acc_coef(lane, i)] = -ac[i];
+    }
+  }
+  for (int j = threadIdx.x; j < NF; j += 64 * W) tws[j] = tb.fft1[j];
+  __syncthreads();
+#pragma unroll 1
+  for (int i = 0; i < N0; ++i) {
+    const int a = __builtin_amdgcn_readfirstlane(la[i]);
+    if (a == 0) continue;  // (X^0 - 1) * ACC = 0 (a is uniform over the workgroup)
+    // GGSW rows of this wave: mask digit `wave` (row wave) and body digit `wave` (row D1 + wave)
+    const double2 *km = bskf + ((size_t)i * 2 * D1 + wave) * 2 * NF + lane * 8;
+    const double2 *kb = bskf + ((size_t)i * 2 * D1 + D1 + wave) * 2 * NF + lane * 8;
+    double2 k[2][2][8];  // [digit row mask/body][output A/B][point]
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      k[0][0][e] = km[e];
+      k[0][1][e] = km[NF + e];
+      k[1][0][e] = kb[e];
+      k[1][1][e] = kb[NF + e];
+    }
+    // digit `wave` of (X^a - 1) * ACC_p for both polys (the shared [ACC, -ACC] extensions)
+    double xr[2][8], xi[2][8];
+    const int base = lane - a + 2 * N1;
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int j = acc_coef(lane, q);
+        const uint32_t w = Lvl1Int::digits(
+            Lvl1Int::canon(ext[p][(base + acc_coef(0, q)) & (2 * N1 - 1)] - ext[p][j]));
+        const double d = Lvl1Int::digit(w, wave);
+        if (q < 8)
+          xr[p][q] = d;
+        else
+          xi[p][q - 8] = d;
+      }
+    F::fwd<2, true>(xr, xi, xch, tws, lane, tb.fft1);
+    double2 o[2][8];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        double re = 0.0, im = 0.0;
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          re = __fma_rn(xr[p][e], k[p][t][e].x, __fma_rn(-xi[p][e], k[p][t][e].y, re));
+          im = __fma_rn(xr[p][e], k[p][t][e].y, __fma_rn(xi[p][e], k[p][t][e].x, im));
+        }
+        o[t][e] = make_double2(re, im);
+      }
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) part[wave][t][e * 64 + lane] = o[t][e];
+    __syncthreads();
+    if (wave < 2) {  // wave 0: output A (mask accumulator), wave 1: output B (body accumulator).
+      // The FFT product is exact after rounding whatever the summation order (device_fft.hpp).
+      double sr[1][8], si[1][8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        double2 s = part[0][wave][e * 64 + lane];
+#pragma unroll
+        for (int w = 1; w < W; ++w) {
+          const double2 v = part[w][wave][e * 64 + lane];
+          s.x += v.x;
+          s.y += v.y;
+        }
+        sr[0][e] = s.x;
+        si[0][e] = s.y;
+      }
+      F::inv<1, true>(sr, si, xch, tws, lane, tb.fft1);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const double v = rint(q < 8 ? sr[0][q] : si[0][q - 8]);  // exact (< 2^43)
+        ac[q] = Lvl1Int::canon(ac[q] + (int)red<Mod<1>>(v));
+        ext[wave][acc_coef(lane, q)] = ac[q];
+        ext[wave][N1 + acc_coef(lane, q)] = -ac[q];
+      }
+    }
+    __syncthreads();
+  }
+  if (mode == 0) {  // extract_lwe_locally (coefficient 0), detector.rs:561
+    uint32_t *o = ext_out + g * (N1 + 1);
+    for (int j = threadIdx.x; j < N1; j += 64 * W) o[j] = Lvl1Int::to_u32(j == 0 ? ext[0][0] : -ext[0][N1 - j]);
+    if (threadIdx.x == 0) o[N1] = Lvl1Int::to_u32(ext[1][0]);
+  } else {
+    uint64_t *o = rlwe_out + g * 2 * N1;
+    for (int j = threadIdx.x; j < N1; j += 64 * W) {
+      o[j] = Lvl1Int::to_u32(ext[0][j]);
+      o[N1 + j] = Lvl1Int::to_u32(ext[1][j]);
+    }
+  }
+}
+
+// ---- level 2 ---------------------------------------------------------------------------------
+// One workgroup of two 256-thread groups per message: group 0 owns the mask accumulator and its
+// 6 digits (GGSW rows 0..5), group 1 the body accumulator and rows 6..11. Per CMUX step each
+// group stages its polynomial, transforms its 6 digits and multiply-accumulates both outputs;
+// group 0 hands its output-B partial to group 1 and group 1 its output-A partial to group 0
+// through `part`; each group then runs one inverse transform. Each group keeps the three-buffer
+// discipline of cmux_step3 on its own buffers (staging X1, digits X0 X1 X0 X1 X0 X1, inverse X0:
+// consecutive cross-wave uses alternate); the workgroup barriers are a superset of the group's,
+// and both groups run the same barrier sequence (a is uniform). Output: the blind rotation in the
+// coefficient domain, u64 [2][N2] (mode 1 of br2_trace_kernel); trace_kernel finishes mode 0.
+constexpr int BR2L_T = 2 * BR2_T;
+
+__global__ __launch_bounds__(BR2L_T, 1) void br2l_kernel(const uint32_t *__restrict__ lwe_int,
+                                                         const double *__restrict__ bsk2, DeviceTables tb,
+                                                         uint64_t *__restrict__ out) {
+  using M = Mod<2>;
+  constexpr int T = BR2_T, E = BR2_E, N = N2;
+  using NTT = WgNtt<M, T, E>;
+  using DG = Digits2;
+  __shared__ double xbuf[2][NTT::LDS3_DOUBLES];
+  __shared__ double part[2][N];
+  __shared__ double tws[N + 136 * 5];  // forward twiddles + the five small-digit stage tables
+  const int g = threadIdx.x / T, t = threadIdx.x % T;
+  double *X = xbuf[g];
+  const double *tw = tws, *t0 = tws + N;
+  const uint32_t *lwe = lwe_int + (size_t)blockIdx.x * (NI + 1);
+  double acc[E];
+  {
+    const int b = (int)lwe[NI];
+    const int rr = (2 * N - (b % (2 * N))) % (2 * N);
+#pragma unroll
+    for (int e = 0; e < E; ++e) acc[e] = g == 1 ? canon_small<M>(rot_read<N>(tb.lut2, t + e * T, rr)) : 0.0;
+    for (int j = threadIdx.x; j < N; j += BR2L_T) tws[j] = tb.tw2[j];
+    if (threadIdx.x <= 128) {  // table k: d * c_k, d = tid - 64 (c = tw1, tw2, tw1 tw2, tw3, tw1 tw3)
+      const double w1 = tb.tw2[1], w2 = tb.tw2[2], w3 = tb.tw2[3];
+      const double c[5] = {w1, w2, canon<M>(mm<M>(w1, w2)), w3, canon<M>(mm<M>(w1, w3))};
+#pragma unroll
+      for (int k = 0; k < 5; ++k)
+        tws[N + 136 * k + threadIdx.x] = canon<M>(mm<M>((double)((int)threadIdx.x - 64), c[k]));
+    }
+    __syncthreads();
+  }
+#pragma unroll 1
+  for (int i = 0; i < NI; ++i) {
+    const int a = (int)__builtin_amdgcn_readfirstlane(lwe[i]) & (2 * N - 1);
+    if (a == 0) continue;  // (X^0 - 1) * ACC = 0
+    const double *ggsw = bsk2 + ((size_t)i * 2 * D2 + (size_t)g * D2) * 2 * N;
+    uint32_t pk[E][DG::DW];
+    {  // digits of (X^a - 1) * ACC_g, staged in X1
+      double *st = X + N;
+#pragma unroll
+      for (int e = 0; e < E; ++e) st[t + e * T] = acc[e];
+      __syncthreads();
+#pragma unroll
+      for (int e = 0; e < E; ++e) DG::pack(canon_small<M>(rot_read<N>(st, t + e * T, a) - acc[e]), pk[e]);
+      __builtin_amdgcn_wave_barrier();
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    }
+    double accA[E], accB[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) accA[e] = accB[e] = 0.0;
+    KeyRow<double, E> cur;
+    cur.load(ggsw, N, t * E);
+#pragma unroll 1
+    for (int k2 = 0; k2 < D2; k2 += 2) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int k = k2 + h;
+        double x[E];
+        int d[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) d[e] = DG::get_int(pk[e], k);
+        if (h == 0)  // digits on X0, X1, X0, ...
+          NTT::template fwd3_small<0>(d, t0, x, X, tw, t);
+        else
+          NTT::template fwd3_small<1>(d, t0, x, X, tw, t);
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          accA[e] += mm<M>(x[e], cur.a[e]);
+          accB[e] += mm<M>(x[e], cur.b[e]);
+        }
+        if (k == 3) {  // four products on a reduced sum stay below 6.5q (cmux_step3)
+#pragma unroll
+          for (int e = 0; e < E; ++e) {
+            accA[e] = red<M>(accA[e]);
+            accB[e] = red<M>(accB[e]);
+          }
+        }
+        if (k + 1 < D2) cur.load(ggsw + (size_t)(k + 1) * 2 * N, N, t * E);
+      }
+    }
+    // exchange the partial the other group owns: group 0 sends B, group 1 sends A
+#pragma unroll
+    for (int e = 0; e < E; ++e) part[1 - g][t * E + e] = red<M>(g == 0 ? accB[e] : accA[e]);
+    __syncthreads();
+    double s[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) s[e] = red<M>(red<M>(g == 0 ? accA[e] : accB[e]) + part[g][t * E + e]);
+    NTT::template inv3m<0>(s, X, tw, t);
+#pragma unroll
+    for (int e = 0; e < E; ++e) acc[e] = canon<M>(acc[e] + s[e]);
+  }
+  uint64_t *o = out + (size_t)blockIdx.x * 2 * N + (size_t)g * N;
+#pragma unroll
+  for (int e = 0; e < E; ++e) o[t + e * T] = to_u64<M>(acc[e]);
+}
+
+// hom_trace (detector.rs:626-639) in place on blind-rotation outputs (coefficient domain,
+// canonical u64 [2][N2] per message) -> NttRlweCiphertext u64 [2][N2].
+__global__ __launch_bounds__(BR2_T, 2) void trace_kernel(uint64_t *__restrict__ io, const double *__restrict__ tk,
+                                                         DeviceTables tb) {
+  using M = Mod<2>;
+  constexpr int T = BR2_T, E = BR2_E, N = N2;
+  using NTT = WgNtt<M, T, E>;
+  __shared__ double xch[NTT::LDS3_DOUBLES];
+  __shared__ double tws[N];
+  const int tid = threadIdx.x;
+  uint64_t *o = io + (size_t)blockIdx.x * 2 * N;
+  double acc0[E], acc1[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    acc0[e] = from_u64<M>(o[tid + e * T]);
+    acc1[e] = from_u64<M>(o[N + tid + e * T]);
+    tws[tid + e * T] = tb.tw2[tid + e * T];
+    xch[2 * N + tid + e * T] = tb.itw2[tid + e * T];
+  }
+  __syncthreads();
+  hom_trace_store(acc0, acc1, xch, tws, xch + 2 * N, tk, tb, o, tid);
+}
+
+}  // namespace omr
+
+#include "ks_mfma.hpp"
+
+namespace omr {
+
+// ---- key switch, split over the input coefficients -------------------------------------------
+constexpr int KS_SPLIT = 32;  // slices of the 1024 input coefficients
+
+// grid (ceil(B / 64), 21, KS_SPLIT): ks_mfma_kernel's tile over input coefficients
+// [z * 1024 / KS_SPLIT, (z + 1) * 1024 / KS_SPLIT); int32 limb sums to part[z][m][col][limb].
+__global__ __launch_bounds__(64, 2) void ks_mfma_split_kernel(const uint32_t *__restrict__ lwe1t,
+                                                           const uint32_t *__restrict__ kskb,
+                                                           int *__restrict__ part, int B, int Bpad) {
+  const int lane = threadIdx.x, r = lane & 31, h = lane >> 5;
+  const int m0 = blockIdx.x * 64, c0 = blockIdx.y * 32, z = blockIdx.z;
+  omr_v16i acc[2][KSM_LIMBS];
+#pragma unroll
+  for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+    for (int l = 0; l < KSM_LIMBS; ++l) acc[tt][l] = omr_v16i{};
+  const bool live0 = m0 + r < B, live1 = m0 + 32 + r < B;
+  const omr_v4i *bbase = reinterpret_cast<const omr_v4i *>(kskb) + (size_t)(c0 + r) * 2 + h;
+  constexpr int SL = N1 / KS_SPLIT;
+#pragma unroll 1
+  for (int i = z * SL; i < (z + 1) * SL; ++i) {
+    const uint32_t x0 = live0 ? lwe1t[(size_t)i * B + m0 + r] : 0u;
+    const uint32_t x1 = live1 ? lwe1t[(size_t)i * B + m0 + 32 + r] : 0u;
+    const omr_v4i a0 = bit_bytes16(x0, 16 * h), a1 = bit_bytes16(x1, 16 * h);
+#pragma unroll
+    for (int l = 0; l < KSM_LIMBS; ++l) {
+      const omr_v4i bv = bbase[((size_t)i * KSM_LIMBS + l) * KSM_COLS * 2];
+      acc[0][l] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, bv, acc[0][l], 0, 0, 0);
+      acc[1][l] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1, bv, acc[1][l], 0, 0, 0);
+    }
+  }
+  const int col = c0 + r;
+#pragma unroll
+  for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const int m = m0 + 32 * tt + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+      int *p = part + (((size_t)z * Bpad + m) * KSM_COLS + col) * KSM_LIMBS;
+#pragma unroll
+      for (int l = 0; l < KSM_LIMBS; ++l) p[l] = acc[tt][l][reg];
+    }
+}
+
+// Sum of the slices and ks_mfma_kernel's epilogue: one thread per (message, output column).
+__global__ void ks_combine_kernel(const int *__restrict__ part, const uint32_t *__restrict__ lwe1t,
+                                  uint32_t *__restrict__ lwe_int, int B, int Bpad) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= B * (NI + 1)) return;
+  const int m = idx / (NI + 1), col = idx % (NI + 1);
+  int64_t limb[KSM_LIMBS] = {0, 0, 0, 0};
+  for (int z = 0; z < KS_SPLIT; ++z) {
+    const int *p = part + (((size_t)z * Bpad + m) * KSM_COLS + col) * KSM_LIMBS;
+#pragma unroll
+    for (int l = 0; l < KSM_LIMBS; ++l) limb[l] += p[l];
+  }
+  const uint64_t sum = (uint64_t)limb[0] + ((uint64_t)limb[1] << 7) + ((uint64_t)limb[2] << 14) +
+                       ((uint64_t)limb[3] << 21);
+  lwe_int[(size_t)m * (NI + 1) + col] = ks_epilogue(sum, lwe1t[(size_t)N1 * B + m], col);
+}
+
+}  // namespace omr

@@ -1,0 +1,26 @@
+"""Single-message (and small-batch) detect latency and its stage split (HIP events), on the
+bench's seeded keys. python tools/latency_split.py [D ...]"""
+import sys
+import time
+
+sys.path.insert(0, "tests")
+import numpy as np  # noqa: E402
+
+import product_lib as PL  # noqa: E402
+from product_lib import omr_amd as A  # noqa: E402
+
+a, b, dk = PL.keys()
+det = A.Detector(dk)
+ca, cb = a.gen_clues(1000, 0, 256)
+det.detect_batch(ca[:4], cb[:4])  # warm
+for D in [int(x) for x in sys.argv[1:]] or [1, 2, 7, 64]:
+    best = None
+    for _ in range(3):
+        t = time.perf_counter()
+        out, info = det.detect_with_time_info(ca[:D], cb[:D])
+        wall = (time.perf_counter() - t) * 1e3
+        if best is None or wall < best[0]:
+            best = (wall, info)
+    w, info = best
+    print(f"D={D}: wall {w:.2f} ms  br1 {info['first_level_ms']:.2f}  ks {info['key_switch_ms']:.3f}  "
+          f"br2+trace {info['second_level_ms']:.2f}  device total {info['total_ms']:.2f}", flush=True)
