@@ -3,9 +3,9 @@
  * See omr_oracle.h for the pinned conventions and the parity status ("unpinned" at the bit
  * level against the reference; pinned by golden vectors + the reference's functional KATs).
  *
- * Written for clarity, not speed: plain loops over u64 residues, Shoup twiddles in the NTT
- * and an 80-bit long-double quotient estimate for other products (both self-checked by the
- * golden-vector tests).
+ * Written for clarity, not speed: plain loops over u64 residues, Shoup twiddles in the NTT,
+ * external-product sums kept exactly in 128 bits and reduced once, and an 80-bit long-double
+ * quotient estimate for other products (all self-checked by the golden-vector tests).
  */
 #include "omr_oracle.h"
 
@@ -324,8 +324,10 @@ static void ext_product(int level, const uint64_t *ca, const uint64_t *cb, const
   const basis_t *bs = &g_basis[level];
   const int N = t->N, d = bs->d;
   const uint64_t q = t->q;
-  uint64_t *acc_a = calloc((size_t)N, sizeof(uint64_t));
-  uint64_t *acc_b = calloc((size_t)N, sizeof(uint64_t));
+  /* the 2d products per coefficient are summed exactly in 128 bits (each < 2^100, 12 of them
+   * < 2^104) and reduced once */
+  u128 *acc_a = calloc((size_t)N, sizeof(u128));
+  u128 *acc_b = calloc((size_t)N, sizeof(u128));
   uint64_t *dig = malloc(sizeof(uint64_t) * (size_t)N * d);
   int64_t tmp[32];
   for (int p = 0; p < 2; ++p) {
@@ -340,15 +342,17 @@ static void ext_product(int level, const uint64_t *ca, const uint64_t *cb, const
       const uint64_t *ga = ggsw + ((size_t)(p * d + k) * 2 + 0) * N;
       const uint64_t *gb = ggsw + ((size_t)(p * d + k) * 2 + 1) * N;
       for (int j = 0; j < N; ++j) {
-        acc_a[j] = addmod(acc_a[j], mulmod(D[j], ga[j], q), q);
-        acc_b[j] = addmod(acc_b[j], mulmod(D[j], gb[j], q), q);
+        acc_a[j] += (u128)D[j] * ga[j];
+        acc_b[j] += (u128)D[j] * gb[j];
       }
     }
   }
-  ntt_inv(t, acc_a);
-  ntt_inv(t, acc_b);
-  memcpy(oa, acc_a, sizeof(uint64_t) * N);
-  memcpy(ob, acc_b, sizeof(uint64_t) * N);
+  for (int j = 0; j < N; ++j) {
+    oa[j] = (uint64_t)(acc_a[j] % q);
+    ob[j] = (uint64_t)(acc_b[j] % q);
+  }
+  ntt_inv(t, oa);
+  ntt_inv(t, ob);
   free(acc_a);
   free(acc_b);
   free(dig);
