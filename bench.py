@@ -211,7 +211,8 @@ def main():
     dev = torch.device("cuda", local)
     if world > 1 or args.force_dist:
         import torch.distributed as dist
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        for k, v in (("MASTER_ADDR", "127.0.0.1"), ("MASTER_PORT", "29511"), ("RANK", "0"), ("WORLD_SIZE", "1")):
+            os.environ.setdefault(k, v)
         dist.init_process_group("nccl", device_id=dev)
     else:
         dist = None
