@@ -73,27 +73,36 @@ std::vector<double> negacyclic_lut(const std::vector<uint64_t> &v, int N, int lo
 
 // FFT twiddles of WgFft<T, E, L> (device_fft.hpp): node i of stage s -> w^(eps(s, i) / 2),
 // w = exp(i pi / 2n), n = 2^L, eps(0, 0) = n, eps(s+1, 2i) = eps(s, i) / 2,
-// eps(s+1, 2i+1) = eps(s, i) / 2 + 2n (mod 4n). Evaluated in long double and rounded once;
-// the last pass's stages stored lane-minor (WgFft::twiddle_index).
+// eps(s+1, 2i+1) = eps(s, i) / 2 + 2n (mod 4n). Radix-8 pass p, block hi: A = node (3p, hi),
+// B = node (3p + 1, 2 hi), C = node (3p + 2, 4 hi); entry t * 8^p - 1 + hi holds T_t of
+// (1, C, B, BC, A, AC, AB, ABC), each an exact angle (sum of the nodes' integer half-eps)
+// evaluated in long double and rounded once.
 std::vector<double2> fft_twiddles(int T, int E, int L) {
+  (void)T;
   const int n = 1 << L, R = __builtin_ctz(E);
-  const int rl = L - ((L + R - 1) / R - 1) * R;  // stages of the last pass
   std::vector<double2> tw(n, make_double2(1.0, 0.0));
+  std::vector<std::vector<int>> half(L);  // half[s][i] = eps(s, i) / 2
   std::vector<int> eps{n};
   for (int s = 0; s < L; ++s) {
     std::vector<int> next;
-    const int k = s - (L - rl);  // stage within the last pass (< 0: earlier pass)
-    const int q = R - rl + k;    // last pass: node = (lane << q) | j
-    for (int i = 0; i < (1 << s); ++i) {
-      const int half = eps[i] / 2;
-      const long double ang =
-          3.14159265358979323846264338327950288L * (long double)half / (long double)(2 * n);
-      const int pos = k < 0 ? (1 << s) + i : (1 << s) + (i & ((1 << q) - 1)) * T + (i >> q);
-      tw[pos] = make_double2((double)cosl(ang), (double)sinl(ang));
-      next.push_back(half % (4 * n));
-      next.push_back((half + 2 * n) % (4 * n));
+    for (int e : eps) {
+      half[s].push_back(e / 2);
+      next.push_back((e / 2) % (4 * n));
+      next.push_back((e / 2 + 2 * n) % (4 * n));
     }
     eps.swap(next);
+  }
+  for (int p = 0; p * R < L; ++p) {
+    const int s0 = p * R, blocks = 1 << s0;
+    for (int hi = 0; hi < blocks; ++hi) {
+      const long a = half[s0][hi], b = half[s0 + 1][2 * hi], c = half[s0 + 2][4 * hi];
+      const long h[8] = {0, c, b, b + c, a, a + c, a + b, a + b + c};
+      for (int t = 1; t < 8; ++t) {
+        const long double ang =
+            3.14159265358979323846264338327950288L * (long double)(h[t] % (8 * n)) / (long double)(2 * n);
+        tw[t * blocks - 1 + hi] = make_double2((double)cosl(ang), (double)sinl(ang));
+      }
+    }
   }
   return tw;
 }

@@ -13,9 +13,9 @@
 // Cooley-Tukey tree on that factorisation (the twist is folded into the twiddles), the inverse a
 // Gentleman-Sande tree with conjugate twiddles, unscaled (the 1/n is folded into the keys).
 // Node i of stage s uses w^(eps(s, i) / 2), eps(0, 0) = n, eps(s+1, 2i) = eps(s, i) / 2,
-// eps(s+1, 2i+1) = eps(s, i) / 2 + 2n (mod 4n); table layout in twiddle_index.
+// eps(s+1, 2i+1) = eps(s, i) / 2 + 2n (mod 4n). Passes are radix-8 blocks of that tree (WgFft::fwd_pass).
 //
-// T lanes hold E complex values each (N = T E), log2(E) radix-2 stages per pass, an LDS exchange
+// T lanes hold E complex values each (N = T E), log2(E) = 3 stages per pass, an LDS exchange
 // between passes (XOR swizzle found by tools/fft_lds_banks.py: no bank conflicts for
 // ds_write_b128 / ds_read_b128), C independent transforms interleaved. One wave per transform.
 //   forward: in  x[e] = coefficient (lane + T e)    out x[e] = transform index (E lane + e)
@@ -74,19 +74,26 @@ struct WgFft {
   static constexpr int BUF = N;  // LDS slots (double2) per transform
   // slot of register e of `lane` in pass p
   __device__ static __forceinline__ int slot(int p, int lane, int e) { return swz(index(p, lane, e)); }
-  // Node twiddle of stage P*R + k for register e. The last pass's stages are stored lane-minor
-  // (entry (1 << s) + j * T + lane holds node (lane << k) + j) so a wave reads consecutive
-  // entries; in earlier passes lanes of a group share (broadcast) entries.
+  // Radix-8 passes. Pass P of a lane works on one block of the twiddle tree: the stage-s0 node
+  // hi = F >> lb with twiddle A, its children (B, i B) and grandchildren (C, i C, w8 C, i w8 C),
+  // w8 = exp(i pi / 4) (node 4 hi + 2 is the even child of node 2 hi + 1: eps / 4 + n). Three radix-2
+  // stages on registers e (pairs (e, e + 4) with A; (e, e + 2) with B / i B; (e, e + 1) with C, i C,
+  // w8 C, i w8 C) equal "multiply x_e by T_e, then a constant 8-point network" with
+  // T = (1, C, B, BC, A, AC, AB, ABC): 7 complex products + 24 complex additions, the factors i
+  // free and w8 folded into FMAs -- 80 FP64 operations instead of 96
+  // (tools/fft_exactness.py checks both forms against the exact product).
+  // Table: entry t * 8^P - 1 + hi holds T_t of block hi of pass P (t = 1..7; 511 entries), so a
+  // pass-2 read is lane-contiguous and pass-0 reads are wave-uniform.
+  static_assert(R == 3 && L % R == 0, "radix-8 passes: every pass has three stages");
+  __device__ static __forceinline__ constexpr int tw_base(int p) { return (1 << (3 * p)) - 1; }
   template <int P>
-  __device__ static __forceinline__ int twiddle_index(int k, int e, int lane) {
-    constexpr int s0 = P * R, r = stages(P), lb = L - s0 - r;
-    const int F = (lane << (R - r)) | (e >> r);
-    const int node = ((F >> lb) << k) | ((e & ((1 << r) - 1)) >> (r - k));
-    if constexpr (P == NPASS - 1) {  // lane-minor: node = (lane << q) | j  ->  (1 << s) + j T + lane
-      const int q = R - r + k;
-      return (1 << (s0 + k)) + (node & ((1 << q) - 1)) * T + lane;
-    }
-    return (1 << (s0 + k)) + node;
+  __device__ static __forceinline__ int block_of(int lane) { return lane >> (L - P * R - R); }
+  template <int P, bool G>
+  __device__ static __forceinline__ double2 block_twiddle(const double2 *tws, const double2 *__restrict__ gtw,
+                                                          int t, int hi) {
+    const int idx = t * (1 << (3 * P)) - 1 + hi;
+    if constexpr (P == 0 && G) return gtw[idx];  // hi == 0: uniform, scalar loads
+    return tws[idx];
   }
 
   // Exchange between passes PF and PT through the wave's LDS buffer (C transforms).
@@ -112,83 +119,120 @@ struct WgFft {
     wave_lds_fence();
   }
 
-  // Pass 0's node index does not depend on the lane (lane >> (L - R) == 0), so its twiddles
-  // are read from the global table with uniform addresses (scalar loads kept in SGPRs) when
-  // gtw is given; later passes read the LDS copy.
-  template <int P, bool G>
-  __device__ static __forceinline__ double2 twiddle(const double2 *tws, const double2 *__restrict__ gtw,
-                                                    int k, int e, int lane) {
-    if constexpr (P == 0 && G) return gtw[(1 << k) + ((e & ((1 << stages(0)) - 1)) >> (stages(0) - k))];
-    return tws[twiddle_index<P>(k, e, lane)];
-  }
+  static constexpr double S8 = 0.70710678118654752440;  // 1 / sqrt(2), w8 = S8 (1 + i)
 
-  // K0: first stage of the pass (a caller that computed stage 0 itself passes 1)
-  template <int P, int C, bool G = false, int K0 = 0>
+  template <int P, int C, bool G = false>
   __device__ static __forceinline__ void fwd_pass(double (&xr)[C][E], double (&xi)[C][E],
                                                   const double2 *tws, int lane,
                                                   const double2 *__restrict__ gtw = nullptr) {
-    constexpr int r = stages(P);
+    const int hi = block_of<P>(lane);
 #pragma unroll
-    for (int k = K0; k < r; ++k) {
-      const int half = 1 << (r - 1 - k);
+    for (int t = 1; t < 8; ++t) {  // x_t *= T_t
+      const double2 w = block_twiddle<P, G>(tws, gtw, t, hi);
 #pragma unroll
-      for (int e = 0; e < E; ++e) {
-        if (e & half) continue;
-        // sibling nodes 2j, 2j + 1 have twiddles w and i w (half-angles of eps and eps + 2n):
-        // odd nodes reuse the even twiddle and apply the factor i by swapping parts (fewer LDS
-        // twiddle reads, no extra arithmetic)
-        const int pb = k >= 1 ? (1 << (r - k)) : 0;
-        const bool odd = (e & pb) != 0;
-        const double2 w = twiddle<P, G>(tws, gtw, k, odd ? (e & ~pb) : e, lane);
-#pragma unroll
-        for (int c = 0; c < C; ++c) {
-          const double vr = __fma_rn(xr[c][e + half], w.x, -xi[c][e + half] * w.y);
-          const double vi = __fma_rn(xr[c][e + half], w.y, xi[c][e + half] * w.x);
-          const double ur = xr[c][e], ui = xi[c][e];
-          xr[c][e] = odd ? ur - vi : ur + vr;  // u + i v  |  u + v
-          xi[c][e] = odd ? ui + vr : ui + vi;
-          xr[c][e + half] = odd ? ur + vi : ur - vr;
-          xi[c][e + half] = odd ? ui - vr : ui - vi;
-        }
+      for (int c = 0; c < C; ++c) {
+        const double r = __fma_rn(xr[c][t], w.x, -xi[c][t] * w.y);
+        const double i = __fma_rn(xr[c][t], w.y, xi[c][t] * w.x);
+        xr[c][t] = r;
+        xi[c][t] = i;
       }
     }
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      double ar[4], ai[4], br[4], bi[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        ar[e] = xr[c][e] + xr[c][e + 4];
+        ai[e] = xi[c][e] + xi[c][e + 4];
+        br[e] = xr[c][e] - xr[c][e + 4];
+        bi[e] = xi[c][e] - xi[c][e + 4];
+      }
+      // c = a0 +- a2, a1 +- a3; d = b0 +- i b2, b1 +- i b3
+      const double c0r = ar[0] + ar[2], c0i = ai[0] + ai[2], c2r = ar[0] - ar[2], c2i = ai[0] - ai[2];
+      const double c1r = ar[1] + ar[3], c1i = ai[1] + ai[3], c3r = ar[1] - ar[3], c3i = ai[1] - ai[3];
+      const double d0r = br[0] - bi[2], d0i = bi[0] + br[2], d2r = br[0] + bi[2], d2i = bi[0] - br[2];
+      const double d1r = br[1] - bi[3], d1i = bi[1] + br[3], d3r = br[1] + bi[3], d3i = bi[1] - br[3];
+      xr[c][0] = c0r + c1r;
+      xi[c][0] = c0i + c1i;
+      xr[c][1] = c0r - c1r;
+      xi[c][1] = c0i - c1i;
+      xr[c][2] = c2r - c3i;  // c2 + i c3
+      xi[c][2] = c2i + c3r;
+      xr[c][3] = c2r + c3i;  // c2 - i c3
+      xi[c][3] = c2i - c3r;
+      const double u = d1r - d1i, v = d1r + d1i;  // w8 d1 = S8 (u + i v)
+      xr[c][4] = __fma_rn(S8, u, d0r);
+      xi[c][4] = __fma_rn(S8, v, d0i);
+      xr[c][5] = __fma_rn(-S8, u, d0r);
+      xi[c][5] = __fma_rn(-S8, v, d0i);
+      const double u3 = d3r + d3i, v3 = d3r - d3i;  // i w8 d3 = S8 (-u3 + i v3)
+      xr[c][6] = __fma_rn(-S8, u3, d2r);
+      xi[c][6] = __fma_rn(S8, v3, d2i);
+      xr[c][7] = __fma_rn(S8, u3, d2r);
+      xi[c][7] = __fma_rn(-S8, v3, d2i);
+    }
   }
+  // Unscaled inverse of fwd_pass (8 x its inverse): the adjoint network, then x_e *= conj(T_e).
   template <int P, int C, bool G = false>
   __device__ static __forceinline__ void inv_pass(double (&xr)[C][E], double (&xi)[C][E],
                                                   const double2 *tws, int lane,
                                                   const double2 *__restrict__ gtw = nullptr) {
-    constexpr int r = stages(P);
+    const int hi = block_of<P>(lane);
 #pragma unroll
-    for (int k = r - 1; k >= 0; --k) {
-      const int half = 1 << (r - 1 - k);
+    for (int c = 0; c < C; ++c) {
+      const double *o_r = xr[c], *o_i = xi[c];
+      const double c0r = o_r[0] + o_r[1], c0i = o_i[0] + o_i[1], c1r = o_r[0] - o_r[1], c1i = o_i[0] - o_i[1];
+      const double c2r = o_r[2] + o_r[3], c2i = o_i[2] + o_i[3];
+      const double c3r = o_i[2] - o_i[3], c3i = o_r[3] - o_r[2];  // -i (o2 - o3)
+      const double d0r = o_r[4] + o_r[5], d0i = o_i[4] + o_i[5];
+      const double ur = o_r[4] - o_r[5], ui = o_i[4] - o_i[5];
+      const double d1r = ur + ui, d1i = ui - ur;  // (1 - i) (o4 - o5) = sqrt 2 conj(w8) (o4 - o5)
+      const double d2r = o_r[6] + o_r[7], d2i = o_i[6] + o_i[7];
+      const double vr = o_r[6] - o_r[7], vi = o_i[6] - o_i[7];
+      const double d3r = vi - vr, d3i = -vr - vi;  // (-1 - i) (o6 - o7) = sqrt 2 conj(i w8) (o6 - o7)
+      const double a0r = c0r + c2r, a0i = c0i + c2i, a2r = c0r - c2r, a2i = c0i - c2i;
+      const double a1r = c1r + c3r, a1i = c1i + c3i, a3r = c1r - c3r, a3i = c1i - c3i;
+      const double b0r = d0r + d2r, b0i = d0i + d2i;
+      const double b2r = d0i - d2i, b2i = d2r - d0r;  // -i (d0 - d2)
+      const double b1r = d1r + d3r, b1i = d1i + d3i;
+      const double b3r = d1i - d3i, b3i = d3r - d1r;  // -i (d1 - d3)
+      xr[c][0] = a0r + b0r;
+      xi[c][0] = a0i + b0i;
+      xr[c][4] = a0r - b0r;
+      xi[c][4] = a0i - b0i;
+      xr[c][2] = a2r + b2r;
+      xi[c][2] = a2i + b2i;
+      xr[c][6] = a2r - b2r;
+      xi[c][6] = a2i - b2i;
+      xr[c][1] = __fma_rn(S8, b1r, a1r);
+      xi[c][1] = __fma_rn(S8, b1i, a1i);
+      xr[c][5] = __fma_rn(-S8, b1r, a1r);
+      xi[c][5] = __fma_rn(-S8, b1i, a1i);
+      xr[c][3] = __fma_rn(S8, b3r, a3r);
+      xi[c][3] = __fma_rn(S8, b3i, a3i);
+      xr[c][7] = __fma_rn(-S8, b3r, a3r);
+      xi[c][7] = __fma_rn(-S8, b3i, a3i);
+    }
 #pragma unroll
-      for (int e = 0; e < E; ++e) {
-        if (e & half) continue;
-        const int pb = k >= 1 ? (1 << (r - k)) : 0;  // see fwd_pass
-        const bool odd = (e & pb) != 0;
-        const double2 w = twiddle<P, G>(tws, gtw, k, odd ? (e & ~pb) : e, lane);
+    for (int t = 1; t < 8; ++t) {  // x_t *= conj(T_t)
+      const double2 w = block_twiddle<P, G>(tws, gtw, t, hi);
 #pragma unroll
-        for (int c = 0; c < C; ++c) {
-          const double ur = xr[c][e], ui = xi[c][e];
-          const double dr = ur - xr[c][e + half], di = ui - xi[c][e + half];
-          xr[c][e] = ur + xr[c][e + half];
-          xi[c][e] = ui + xi[c][e + half];
-          // (dr + i di) * conj(w); odd node: conj(i w) = -i conj(w)
-          const double tr = __fma_rn(dr, w.x, di * w.y), ti = __fma_rn(di, w.x, -dr * w.y);
-          xr[c][e + half] = odd ? ti : tr;
-          xi[c][e + half] = odd ? -tr : ti;
-        }
+      for (int c = 0; c < C; ++c) {
+        const double r = __fma_rn(xr[c][t], w.x, xi[c][t] * w.y);
+        const double i = __fma_rn(xi[c][t], w.x, -xr[c][t] * w.y);
+        xr[c][t] = r;
+        xi[c][t] = i;
       }
     }
   }
   // C transforms at once (lds holds C * BUF complex)
   // G: pass-0 twiddles from the global table gtw (must be non-null)
-  template <int C, bool G = false, int K0 = 0>
+  template <int C, bool G = false>
   __device__ static __forceinline__ void fwd(double (&xr)[C][E], double (&xi)[C][E], double2 *lds,
                                              const double2 *tws, int lane,
                                              const double2 *__restrict__ gtw = nullptr) {
     static_assert(NPASS <= 5, "unrolled for up to 5 passes");
-    fwd_pass<0, C, G, K0>(xr, xi, tws, lane, gtw);
+    fwd_pass<0, C, G>(xr, xi, tws, lane, gtw);
 #define OMR_FFT_FWD_STEP(P)                                                                   \
   if constexpr (NPASS > P) {                                                                  \
     constexpr int Q = NPASS > P ? P : 1;                                                      \

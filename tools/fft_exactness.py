@@ -1,8 +1,9 @@
-"""Lane-exact model of the workgroup FFTs (tfhe-omr_amd/csrc/device_fft.hpp, any T x E, partial
-last pass included): checks that the twiddle tree, pass indexing and swizzle reproduce the
-negacyclic product exactly after rounding, reports the worst rounding error for random and
-adversarial digits, and checks that two geometries of one size agree on the transform order
-(keys transformed by one can be used by the other).
+"""Lane-exact model of the workgroup FFTs (tfhe-omr_amd/csrc/device_fft.hpp): checks that the
+twiddle tree, pass indexing and swizzle reproduce the negacyclic product exactly after rounding,
+reports the worst rounding error for random and adversarial digits, and checks that geometries
+of one size agree on the transform order (keys transformed by one can be used by the other).
+Level 1 runs the kernel's radix-8 passes (Fft8: premultiply by T_e, constant 8-point network)
+next to the plain radix-2 stages (Fft); level 2 (a 2-limb FFT, not in the product) radix-2 only.
     python tools/fft_exactness.py            # level 1 (64 x 8, N = 1024)
     python tools/fft_exactness.py --level 2  # level 2 (256 x 4 and 64 x 16, N = 2048, 2 limbs)"""
 import sys
@@ -99,6 +100,56 @@ class Fft:
         return z
 
 
+S8 = np.sqrt(0.5)
+
+
+class Fft8(Fft):
+    """Radix-8 passes as in WgFft::fwd_pass / inv_pass (L a multiple of 3)."""
+
+    def block_tw(self, p):
+        s0, hi = 3 * p, self.lane >> (self.L - 3 * p - 3)
+        A, B, C = self.tw[(1 << s0) + hi], self.tw[(2 << s0) + 2 * hi], self.tw[(4 << s0) + 4 * hi]
+        return [1, C, B, B * C, A, A * C, A * B, A * B * C]
+
+    def fwd(self, z):
+        x = np.stack([z[self.lane + self.T * e] for e in range(self.E)], axis=1).astype(np.complex128)
+        for p in range(self.NP):
+            if p:
+                x = self.exchange(x, p - 1, p)
+            T = self.block_tw(p)
+            P = [x[:, e] * T[e] for e in range(8)]
+            a = [P[e] + P[e + 4] for e in range(4)]
+            b = [P[e] - P[e + 4] for e in range(4)]
+            c0, c2, c1, c3 = a[0] + a[2], a[0] - a[2], a[1] + a[3], a[1] - a[3]
+            d0, d2, d1, d3 = b[0] + 1j * b[2], b[0] - 1j * b[2], b[1] + 1j * b[3], b[1] - 1j * b[3]
+            w8 = S8 * (1 + 1j)
+            x = np.stack([c0 + c1, c0 - c1, c2 + 1j * c3, c2 - 1j * c3, d0 + w8 * d1, d0 - w8 * d1,
+                          d2 + 1j * w8 * d3, d2 - 1j * w8 * d3], axis=1)
+        out = np.zeros(self.n, dtype=np.complex128)
+        for e in range(self.E):
+            out[self.index(self.NP - 1, e)] = x[:, e]
+        return out
+
+    def inv(self, X):
+        x = np.stack([X[self.index(self.NP - 1, e)] for e in range(self.E)], axis=1).astype(np.complex128)
+        for p in range(self.NP - 1, -1, -1):
+            if p < self.NP - 1:
+                x = self.exchange(x, p + 1, p)
+            T = self.block_tw(p)
+            o = [x[:, e] for e in range(8)]
+            c0, c1, c2, c3 = o[0] + o[1], o[0] - o[1], o[2] + o[3], -1j * (o[2] - o[3])
+            d0, d1 = o[4] + o[5], (1 - 1j) * (o[4] - o[5])
+            d2, d3 = o[6] + o[7], (-1 - 1j) * (o[6] - o[7])
+            a0, a2, a1, a3 = c0 + c2, c0 - c2, c1 + c3, c1 - c3
+            b0, b2, b1, b3 = d0 + d2, -1j * (d0 - d2), d1 + d3, -1j * (d1 - d3)
+            P = [a0 + b0, a1 + S8 * b1, a2 + b2, a3 + S8 * b3, a0 - b0, a1 - S8 * b1, a2 - b2, a3 - S8 * b3]
+            x = np.stack([P[e] * np.conj(T[e]) for e in range(8)], axis=1)
+        z = np.zeros(self.n, dtype=np.complex128)
+        for e in range(self.E):
+            z[self.lane + self.T * e] = x[:, e]
+        return z
+
+
 def fold(p):
     h = len(p) // 2
     return p[:h] + 1j * p[h:]
@@ -126,9 +177,9 @@ def adversarial(keys, dmax, N, rng):
     return out
 
 
-def run(geoms, N, kbits, dmax, rows, trials=4):
+def run(geoms, N, kbits, dmax, rows, trials=4, radix8=False):
     rng = np.random.default_rng(5)
-    ffts = [Fft(*g) for g in geoms]
+    ffts = [Fft(*g) for g in geoms] + ([Fft8(*g) for g in geoms] if radix8 else [])
     worst = 0.0
     for trial in range(trials):
         keys = [rng.integers(-(1 << (kbits - 1)), 1 << (kbits - 1), N) for _ in range(rows)]
@@ -153,4 +204,4 @@ if __name__ == "__main__":
     if "--level" in sys.argv and sys.argv[sys.argv.index("--level") + 1] == "2":
         run([(256, 4, 10), (64, 16, 10)], 2048, 25, 64, 12)
     else:
-        run([(64, 8, 9)], 1024, 27, 17, 8)
+        run([(64, 8, 9)], 1024, 27, 17, 8, trials=8, radix8=True)
