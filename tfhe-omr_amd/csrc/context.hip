@@ -120,7 +120,7 @@ struct omr_ctx {
   double2 *fft1 = nullptr;   // level-1 FFT twiddles
   double *bsk2 = nullptr, *tk = nullptr;
   uint32_t *kskb = nullptr;  // int8 limbs of the KSK, [1024][4][672][32] (matrix-core key switch)
-  double *tables = nullptr;  // tw1 itw1 tw2 itw2 lut1 lut2
+  double *tables = nullptr;  // tw1 itw1 tw2 itw2 lut1 lut2 tw2c
   uint16_t *trace_tabs = nullptr;
   DeviceTables tb{};
   size_t batch = OMR_DEFAULT_BATCH, batch_cap = 0;
@@ -219,6 +219,46 @@ omr_status convert_keys(const IN *host, size_t npoly, OUT *dev, double scale, co
     const size_t n = std::min(chunk, npoly - p0);
     HIP_TRY(hipMemcpyAsync(tmp, host + p0 * N, n * N * sizeof(IN), hipMemcpyDefault, st));
     key_to_ntt_kernel<LEVEL, IN, OUT><<<n, T, 0, st>>>(tmp, dev + p0 * N, n, scale, tw);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(st));
+  }
+  dev_free(tmp);
+  return OMR_OK;
+}
+
+// ---- BSK2 rows -> the CmuxNtt forward order, x scale (the blind rotation's key layout) ----
+__global__ __launch_bounds__(256) static void key_to_cmux_kernel(const uint64_t *in, double *out, size_t npoly,
+                                                        double scale, const double *tw2c) {
+  using M = Mod<2>;
+  using NTT = CmuxNtt;
+  __shared__ double lds[NTT::LDS_DOUBLES];
+  __shared__ double tws[NTT::N];
+  const size_t poly = blockIdx.x;
+  const int tid = threadIdx.x;
+  if (poly >= npoly) return;
+  const uint64_t *src = in + poly * NTT::N;
+  double x[NTT::E];
+#pragma unroll
+  for (int e = 0; e < NTT::E; ++e) {
+    x[e] = from_u64<M>(src[tid + e * NTT::T]);
+    tws[tid + e * NTT::T] = tw2c[tid + e * NTT::T];
+  }
+  __syncthreads();
+  NTT::fwd<0>(x, lds, tws, tid);
+  double *dst = out + poly * NTT::N + tid * NTT::E;
+#pragma unroll
+  for (int e = 0; e < NTT::E; ++e) dst[e] = canon<M>(mm<M>(canon<M>(x[e]), scale));
+}
+
+omr_status convert_keys_cmux(const uint64_t *host, size_t npoly, double *dev, double scale, const double *tw2c,
+                             hipStream_t st) {
+  const size_t chunk = 4096;  // polynomials per upload
+  uint64_t *tmp = nullptr;
+  HIP_TRY(hipMalloc(&tmp, chunk * N2 * sizeof(uint64_t)));
+  for (size_t p0 = 0; p0 < npoly; p0 += chunk) {
+    const size_t n = std::min(chunk, npoly - p0);
+    HIP_TRY(hipMemcpyAsync(tmp, host + p0 * N2, n * N2 * sizeof(uint64_t), hipMemcpyDefault, st));
+    key_to_cmux_kernel<<<n, CmuxNtt::T, 0, st>>>(tmp, dev + p0 * N2, n, scale, tw2c);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(st));
   }
@@ -326,8 +366,14 @@ extern "C" omr_status omr_ctx_create(const omr_detection_key_view *key, int devi
   std::vector<uint64_t> v2(TI, 0);
   v2[2 * CLUES] = (2 * Q2 + P) / (2 * P);  // round_half_up(q2/257), detector.rs:479-503
   auto lut2 = negacyclic_lut(v2, N2, 5, Q2);
+  std::vector<double> tw2c(tw2);  // CmuxNtt: stage-9/10 twiddles at their lane-contiguous positions
+  for (int st = 9; st <= 10; ++st)
+    for (int t = 0; t < CmuxNtt::T; ++t)
+      for (int e = 0; e < CmuxNtt::E; ++e)
+        if (!(e & (st == 9 ? 4 : 2)))
+          tw2c[(1 << st) + cmux_tw_off(3, st, t, e)] = tw2[(1 << st) + (cmux_idx(3, t, e) >> (11 - st))];
   std::vector<double> tabs;
-  for (auto *v : {&tw1, &itw1, &tw2, &itw2, &lut1, &lut2}) tabs.insert(tabs.end(), v->begin(), v->end());
+  for (auto *v : {&tw1, &itw1, &tw2, &itw2, &lut1, &lut2, &tw2c}) tabs.insert(tabs.end(), v->begin(), v->end());
   std::vector<uint16_t> ttab(2 * TRACE_STEPS * N2);
   for (int k = 0; k < TRACE_STEPS; ++k) {
     const uint32_t g = (uint32_t)(N2 >> k) + 1;
@@ -354,6 +400,7 @@ extern "C" omr_status omr_ctx_create(const omr_detection_key_view *key, int devi
   c->tb.itw2 = c->tables + 2 * N1 + N2;
   c->tb.lut1 = c->tables + 2 * N1 + 2 * N2;
   c->tb.lut2 = c->tables + 3 * N1 + 2 * N2;
+  c->tb.tw2c = c->tables + 3 * N1 + 3 * N2;
   c->tb.trace_src = c->trace_tabs;
   c->tb.trace_perm = c->trace_tabs + TRACE_STEPS * N2;
   const auto ftw = fft_twiddles(Fft512::T, Fft512::E, Fft512::L);
@@ -372,8 +419,7 @@ extern "C" omr_status omr_ctx_create(const omr_detection_key_view *key, int devi
   omr_status st;
   if ((st = convert_keys_fft1(key->bsk1, BSK1_ELEMS / N1, c->bsk1f, c->fft1, c->stream)) != OMR_OK)
     return fail(st);
-  if ((st = convert_keys<2, uint64_t, double>(key->bsk2, BSK2_ELEMS / N2, c->bsk2, ninv2, c->tb.tw2,
-                                              c->stream)) != OMR_OK)
+  if ((st = convert_keys_cmux(key->bsk2, BSK2_ELEMS / N2, c->bsk2, ninv2, c->tb.tw2c, c->stream)) != OMR_OK)
     return fail(st);
   if ((st = convert_keys<2, uint64_t, double>(key->trace_key, TK_ELEMS / N2, c->tk, 1.0, c->tb.tw2,
                                               c->stream)) != OMR_OK)

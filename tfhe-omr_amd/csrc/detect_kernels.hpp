@@ -97,8 +97,8 @@ struct KeyRow {
 // One CMUX step of the level-2 binary blind rotation (BlindRotationKey::blind_rotate):
 //   ACC += ((X^a - 1) * ACC) [x] GGSW_i
 // acc0/acc1: mask / body accumulator, coefficient tid + e*T, canonical, in registers. ggsw: the
-// NTT-domain rows [2D][2][N], pre-scaled by N^-1. Three-buffer exchanges (xch holds
-// WgNtt::LDS3_DOUBLES).
+// NTT-domain rows [2D][2][N] in the CmuxNtt output order, pre-scaled by N^-1. Three-buffer
+// exchanges (xch holds CmuxNtt::LDS_DOUBLES), tw the permuted table tw2c.
 // Cross-wave uses of the LDS per step, in order: staging of the mask in X1, the 6 mask-digit
 // NTTs on X0, X1, X0, X1, X0, X1, staging of the body in X0, the 6 body-digit NTTs on X1, X0,
 // ..., X0, the inverse A on X1 and B on X0; the step starts on X1 and ends on X0. Consecutive
@@ -110,9 +110,10 @@ __device__ __forceinline__ void cmux_step3(double (&acc0)[E], double (&acc1)[E],
                                            const KeyT *__restrict__ ggsw, const double *tw, int tid,
                                            const double *t0) {
   using M = Mod<2>;
-  using NTT = WgNtt<M, T, E>;
+  using NTT = CmuxNtt;
   using DG = Digits2;
   constexpr int N = M::N;
+  static_assert(T == NTT::T && E == NTT::E, "CMUX transform geometry");
   static_assert(D2 % 2 == 0, "digit loop unrolled by two (alternating cross-wave buffers)");
   double accA[E], accB[E];
 #pragma unroll
@@ -143,9 +144,9 @@ __device__ __forceinline__ void cmux_step3(double (&acc0)[E], double (&acc1)[E],
 #pragma unroll
         for (int e = 0; e < E; ++e) d[e] = DG::get_int(pk[e], k);
         if ((h ^ p) == 0)  // mask digits on X0, X1, ...; body digits on X1, X0, ...
-          NTT::template fwd3_small<0>(d, t0, x, xch, tw, tid);
+          NTT::template fwd_small<0>(d, t0, x, xch, tw, tid);
         else
-          NTT::template fwd3_small<1>(d, t0, x, xch, tw, tid);
+          NTT::template fwd_small<1>(d, t0, x, xch, tw, tid);
 #pragma unroll
         for (int e = 0; e < E; ++e) {
           accA[e] += mm<M>(x[e], (double)cur.a[e]);
@@ -169,10 +170,10 @@ __device__ __forceinline__ void cmux_step3(double (&acc0)[E], double (&acc1)[E],
     accA[e] = red<M>(accA[e]);
     accB[e] = red<M>(accB[e]);
   }
-  NTT::template inv3m<1>(accA, xch, tw, tid);
+  NTT::template inv<1>(accA, xch, tw, tid);
 #pragma unroll
   for (int e = 0; e < E; ++e) acc0[e] = canon<M>(acc0[e] + accA[e]);
-  NTT::template inv3m<0>(accB, xch, tw, tid);
+  NTT::template inv<0>(accB, xch, tw, tid);
 #pragma unroll
   for (int e = 0; e < E; ++e) acc1[e] = canon<M>(acc1[e] + accB[e]);
 }
@@ -316,7 +317,7 @@ __global__ __launch_bounds__(BR2_T, BR2_WAVES) void br2_trace_kernel(const uint3
       const int j = tid + e * T;
       acc0[e] = 0.0;
       acc1[e] = canon_small<M>(rot_read<N>(tb.lut2, j, rr));
-      tws[j] = tb.tw2[j];
+      tws[j] = tb.tw2c[j];  // CMUX transforms: stages 9, 10 permuted (CmuxNtt)
     }
     if (tid <= 128) {  // table k: d * c_k, d = tid - 64 (c = tw1, tw2, tw1 tw2, tw3, tw1 tw3)
       const double w1 = tb.tw2[1], w2 = tb.tw2[2], w3 = tb.tw2[3];
@@ -344,7 +345,10 @@ __global__ __launch_bounds__(BR2_T, BR2_WAVES) void br2_trace_kernel(const uint3
   __syncthreads();  // the last inverse's cross-wave reads of X0 are done everywhere
   double *itw_t = xch + 2 * N;  // the trace's inverse table goes to the W buffer
 #pragma unroll
-  for (int e = 0; e < E; ++e) itw_t[tid + e * T] = tb.itw2[tid + e * T];
+  for (int e = 0; e < E; ++e) {
+    itw_t[tid + e * T] = tb.itw2[tid + e * T];
+    tws[tid + e * T] = tb.tw2[tid + e * T];  // the trace's (generic) transforms read tw2
+  }
   __syncthreads();
   hom_trace_store(acc0, acc1, xch, tw, itw_t, tk, tb, o, tid);
 }

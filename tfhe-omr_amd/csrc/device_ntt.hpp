@@ -12,6 +12,23 @@
 
 namespace omr {
 
+// Exchange register bit r of a pair (a = x[e], b = x[e | 1 << r]) with lane bit LB (5: lanes
+// 32..63 of a <-> lanes 0..31 of b, v_permlane32_swap; 4: odd 16-lane rows of a <-> even rows of
+// b, v_permlane16_swap): afterwards a holds the lane-bit-0 half and lane bit LB indexes the old
+// register bit. One instruction per dword pair.
+template <int LB>
+__device__ __forceinline__ void swap_lane_bit(double &a, double &b) {
+  static_assert(LB == 4 || LB == 5, "lane bits 4 and 5 have swap instructions");
+  const uint64_t ua = __builtin_bit_cast(uint64_t, a), ub = __builtin_bit_cast(uint64_t, b);
+  const uint32_t alo = (uint32_t)ua, ahi = (uint32_t)(ua >> 32), blo = (uint32_t)ub, bhi = (uint32_t)(ub >> 32);
+  const auto lo = LB == 5 ? __builtin_amdgcn_permlane32_swap(alo, blo, false, false)
+                          : __builtin_amdgcn_permlane16_swap(alo, blo, false, false);
+  const auto hi = LB == 5 ? __builtin_amdgcn_permlane32_swap(ahi, bhi, false, false)
+                          : __builtin_amdgcn_permlane16_swap(ahi, bhi, false, false);
+  a = __builtin_bit_cast(double, (uint64_t)lo[0] | ((uint64_t)hi[0] << 32));
+  b = __builtin_bit_cast(double, (uint64_t)lo[1] | ((uint64_t)hi[1] << 32));
+}
+
 template <int LEVEL>
 struct Mod;
 template <>
@@ -272,53 +289,152 @@ struct WgNtt {
     inv_fromC<NPASS - 1, C>(x, lds, itw, tid, since_red);
   }
 
-  // ---- three-buffer single transforms (level-2 CMUX step) -------------------------------------------
-  // Cross-wave exchanges use X0 = lds or X1 = lds + N as the caller chooses (XB), wave-local ones
-  // W = lds + 2N, where each wave only ever touches its own slots (the index set a wave owns in
-  // a wave-local pass pair is the same for every such pair). A caller that alternates X0 / X1
-  // between consecutive cross-wave uses of the LDS never writes a buffer that a slower wave may
-  // still read: the other buffer's barrier separates them. No exchange then needs a trailing
-  // barrier, and a transform costs one workgroup barrier (its one cross-wave exchange).
+  // three exchange buffers of the level-2 CMUX transforms (CmuxNtt) and the trace
   static constexpr int LDS3_DOUBLES = 3 * N;
+  // Single-transform API.
+  __device__ static __forceinline__ void fwd(double (&x)[E], double *lds, const double *tw, int tid) {
+    fwdC<1>(reinterpret_cast<double(&)[1][E]>(x), lds, tw, tid);
+  }
+  __device__ static __forceinline__ void inv(double (&x)[E], double *lds, const double *itw, int tid) {
+    invC<1>(reinterpret_cast<double(&)[1][E]>(x), lds, itw, tid);
+  }
+};
+
+
+// ------------------------------------------------------------------------------------------
+// Level-2 CMUX transforms (256 threads x 8 residues, N2 = 2048): the digit NTTs, inverse NTTs
+// and BSK2 conversion of the blind rotation. Index bits 10..0 (stage s splits on bit 10 - s)
+// are processed in four passes; cidx(p, tid, e) is the index register e of thread tid holds:
+//   P0: e -> 10..8, tid 7..0 -> 7..0                   (the coefficient layout tid + 256 e)
+//   P1: e -> 7..5, tid 7..5 -> 10..8, tid 4..0 -> 4..0 (cross-wave LDS exchange from P0)
+//   P2: e -> 4..2, tid 7,6 -> 10,9, tid 3..0 -> 8..5, tid 5 -> 1, tid 4 -> 0 (wave-local LDS)
+//   P3: register bits 2,1 <-> lane bits 5,4 of P2 by v_permlane32_swap / v_permlane16_swap
+//       (e2 -> 1, e1 -> 0, e0 -> 2, tid 5 -> 4, tid 4 -> 3): no LDS, 16 swaps per transform.
+// Stage-9 and -10 twiddles are read lane-contiguously from the permuted table tw2c (a bit
+// permutation of each stage's node index, so the mirrored inverse lookup (2 << s) - 1 - pos holds
+// unchanged); stages 0..8 of tw2c equal tw2. The forward output (and BSK2) sits at register e of
+// thread tid = position tid * 8 + e, NTT index cidx(3, tid, e).
+// Exchange buffers (LDS3_DOUBLES): X0 = lds, X1 = lds + N for the cross-wave exchange (the
+// caller alternates them, as the staging does), W = lds + 2N for the wave-local one (each wave
+// only touches the slots of its own index bits 10, 9).
+// ------------------------------------------------------------------------------------------
+OMR_HD constexpr int cmux_idx(int p, int tid, int e) {
+  return p == 0   ? (e << 8) | tid
+         : p == 1 ? ((tid >> 5) << 8) | (e << 5) | (tid & 31)
+         : p == 2 ? ((tid >> 6) << 9) | ((tid & 15) << 5) | (e << 2) | (((tid >> 5) & 1) << 1) | ((tid >> 4) & 1)
+                  : ((tid >> 6) << 9) | ((tid & 15) << 5) | (((tid >> 5) & 1) << 4) | (((tid >> 4) & 1) << 3) |
+                        ((e & 1) << 2) | (((e >> 2) & 1) << 1) | ((e >> 1) & 1);
+}
+// offset of the stage-s twiddle (within the stage's 2^s entries) of the pair whose lower register
+// is e: the node index for s <= 8, the permuted position for s = 9, 10
+OMR_HD constexpr int cmux_tw_off(int p, int s, int tid, int e) {
+  return s == 9    ? (e & 1) * 256 + tid
+         : s == 10 ? ((((e >> 2) & 1) << 1) | (e & 1)) * 256 + tid
+                   : cmux_idx(p, tid, e) >> (11 - s);
+}
+
+struct CmuxNtt {
+  using M = Mod<2>;
+  static constexpr int T = 256, E = 8, N = 2048, L = 11;
+  using G = WgNtt<M, T, E>;
+  static_assert(N == M::N, "level-2 geometry");
+  static constexpr int LDS_DOUBLES = 3 * N;
+  // register bit holding index bit b in pass p
+  static constexpr int rbit(int p, int b) { return p == 0 ? b - 8 : p == 1 ? b - 5 : p == 2 ? b - 2 : (b == 1 ? 2 : 1); }
+  // W-buffer swizzle: index bits 5..8 into slot bits 1..4 and bit 8 into bit 0 -- conflict free for
+  // ds_write_b64 / ds_read_b64 in both P1 and P2 layouts (tests/test_cmux_layout.py)
+  __device__ static __forceinline__ int padw(int j) { return j ^ (((j >> 5) & 15) << 1) ^ ((j >> 8) & 1); }
+
+  template <int P, int S, bool INV>
+  __device__ static __forceinline__ void stage(double (&x)[E], const double *tw, int tid, int &since_red) {
+    constexpr int h = 1 << rbit(P, L - 1 - S);
+    if (since_red >= (INV ? M::RED_INV : M::RED_FWD)) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) x[e] = red<M>(x[e]);
+      since_red = 0;
+    }
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      if (e & h) continue;
+      const int off = cmux_tw_off(P, S, tid, e);
+      if constexpr (!INV) {
+        const double w = tw[(1 << S) + off];
+        const double u = x[e], v = mm<M>(x[e + h], w);
+        x[e] = u + v;
+        x[e + h] = u - v;
+      } else {  // psi^-brv(2^s + j) = -psi^brv(2^(s+1) - 1 - j): the forward table mirrored
+        const double w = tw[(2 << S) - 1 - off];
+        const double u = x[e], v = x[e + h];
+        x[e] = u + v;
+        x[e + h] = mm<M>(v - u, w);
+      }
+    }
+    ++since_red;
+  }
+  template <int P, int S0, int S1>
+  __device__ static __forceinline__ void fwd_stages(double (&x)[E], const double *tw, int tid, int &since_red) {
+    if constexpr (S0 < S1) {
+      stage<P, S0, false>(x, tw, tid, since_red);
+      fwd_stages<P, S0 + 1, S1>(x, tw, tid, since_red);
+    }
+  }
+  template <int P, int S0, int S1>  // stages S1 - 1 down to S0
+  __device__ static __forceinline__ void inv_stages(double (&x)[E], const double *tw, int tid, int &since_red) {
+    if constexpr (S0 < S1) {
+      stage<P, S1 - 1, true>(x, tw, tid, since_red);
+      inv_stages<P, S0, S1 - 1>(x, tw, tid, since_red);
+    }
+  }
+  // cross-wave exchange P0 <-> P1 through X0 / X1 (no trailing barrier: see the buffer rule)
   template <int PF, int PT, int XB>
-  __device__ static __forceinline__ void exchange3(double (&x)[E], double *lds, int tid) {
-    constexpr bool WL = wave_local(PF, PT);
-    double *buf = lds + (WL ? 2 : XB) * N;
+  __device__ static __forceinline__ void exchange_x(double (&x)[E], double *lds, int tid) {
+    double *buf = lds + XB * N;
 #pragma unroll
-    for (int e = 0; e < E; ++e) buf[pad(index(PF, tid, e))] = x[e];
-    if constexpr (WL)
-      wave_sync();
-    else
-      __syncthreads();
+    for (int e = 0; e < E; ++e) buf[G::pad(cmux_idx(PF, tid, e))] = x[e];
+    __syncthreads();
 #pragma unroll
-    for (int e = 0; e < E; ++e) x[e] = buf[pad(index(PT, tid, e))];
-    // a wave's own LDS operations complete in order; only keep the compiler from hoisting the
-    // next exchange's writes above these reads
+    for (int e = 0; e < E; ++e) x[e] = buf[G::pad(cmux_idx(PT, tid, e))];
+    __builtin_amdgcn_wave_barrier();  // keep the next writes below these reads (in-order LDS)
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  }
+  // wave-local exchange P1 <-> P2 through W
+  template <int PF, int PT>
+  __device__ static __forceinline__ void exchange_w(double (&x)[E], double *lds, int tid) {
+    double *buf = lds + 2 * N;
+#pragma unroll
+    for (int e = 0; e < E; ++e) buf[padw(cmux_idx(PF, tid, e))] = x[e];
+    G::wave_sync();
+#pragma unroll
+    for (int e = 0; e < E; ++e) x[e] = buf[padw(cmux_idx(PT, tid, e))];
     __builtin_amdgcn_wave_barrier();
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
   }
-  static constexpr int cross_wave_exchanges() {
-    int n = 0;
-    for (int p = 1; p < NPASS; ++p) n += wave_local(p - 1, p) ? 0 : 1;
-    return n;
+  // P2 <-> P3: register bit 2 <-> lane bit 5, register bit 1 <-> lane bit 4 (an involution)
+  __device__ static __forceinline__ void swap23(double (&x)[E]) {
+#pragma unroll
+    for (int e = 0; e < E; ++e)
+      if (!(e & 4)) swap_lane_bit<5>(x[e], x[e + 4]);
+#pragma unroll
+    for (int e = 0; e < E; ++e)
+      if (!(e & 2)) swap_lane_bit<4>(x[e], x[e + 2]);
   }
-  template <int P, int XB>
-  __device__ static __forceinline__ void fwd3_from(double (&x)[E], double *lds, const double *tw,
-                                                   int tid, int &since_red) {
-    if constexpr (P < NPASS) {
-      if constexpr (P > 0) exchange3<P - 1, P, XB>(x, lds, tid);
-      fwd_passC<P, 1>(reinterpret_cast<double(&)[1][E]>(x), tw, tid, since_red);
-      fwd3_from<P + 1, XB>(x, lds, tw, tid, since_red);
-    }
+  // passes 1..3 of the forward transform after pass 0 (stages 0..2) is done
+  template <int XB>
+  __device__ static __forceinline__ void fwd_rest(double (&x)[E], double *lds, const double *tw, int tid,
+                                                  int &since_red) {
+    exchange_x<0, 1, XB>(x, lds, tid);
+    fwd_stages<1, 3, 6>(x, tw, tid, since_red);
+    exchange_w<1, 2>(x, lds, tid);
+    fwd_stages<2, 6, 9>(x, tw, tid, since_red);
+    swap23(x);
+    fwd_stages<3, 9, 11>(x, tw, tid, since_red);
   }
-  template <int P, int XB, bool MIRROR = false>
-  __device__ static __forceinline__ void inv3_from(double (&x)[E], double *lds, const double *itw,
-                                                   int tid, int &since_red) {
-    if constexpr (P >= 0) {
-      if constexpr (P < NPASS - 1) exchange3<P + 1, P, XB>(x, lds, tid);
-      inv_passC<P, 1, MIRROR>(reinterpret_cast<double(&)[1][E]>(x), itw, tid, since_red);
-      inv3_from<P - 1, XB, MIRROR>(x, lds, itw, tid, since_red);
-    }
+  // forward transform of arbitrary residues |x| <= q/2 (key conversion)
+  template <int XB>
+  __device__ static __forceinline__ void fwd(double (&x)[E], double *lds, const double *tw, int tid) {
+    int since_red = 0;
+    fwd_stages<0, 0, 3>(x, tw, tid, since_red);
+    fwd_rest<XB>(x, lds, tw, tid, since_red);
   }
   // Forward transform of a polynomial of small integer digits |d| <= 64: stages 0 and 1 from
   // five 129-entry LDS tables (t0 + 136 k: d * c_k for c = tw1, tw2, tw1 tw2, tw3, tw1 tw3)
@@ -328,9 +444,8 @@ struct WgNtt {
   // (1.7q with the products), 6.84q before the stage-6 reduction: below 8q < 2^53 and inside mm's
   // exact range (replayed in tests/test_fp64_residues.py).
   template <int XB>
-  __device__ static __forceinline__ void fwd3_small(const int (&d)[E], const double *t0, double (&x)[E],
-                                                    double *lds, const double *tw, int tid) {
-    static_assert(R == 3 && T == (1 << (L - R)), "stage tables written for full radix-8 first passes");
+  __device__ static __forceinline__ void fwd_small(const int (&d)[E], const double *t0, double (&x)[E],
+                                                   double *lds, const double *tw, int tid) {
     const double *T1 = t0, *T2 = t0 + 136, *T3 = t0 + 272, *T4 = t0 + 408, *T5 = t0 + 544;
     const double a4 = T1[d[4] + 64], a5 = T1[d[5] + 64];
     const double x0 = (double)d[0] + a4, x4 = (double)d[0] - a4;
@@ -346,22 +461,20 @@ struct WgNtt {
     x[5] = x5 + v5;
     x[7] = x5 - v5;
     int since_red = 2;
-    fwd_passC<0, 1, 2>(reinterpret_cast<double(&)[1][E]>(x), tw, tid, since_red);
-    fwd3_from<1, XB>(x, lds, tw, tid, since_red);
+    fwd_stages<0, 2, 3>(x, tw, tid, since_red);
+    fwd_rest<XB>(x, lds, tw, tid, since_red);
   }
-  // Inverse with the forward table mirrored (MIRROR in inv_passC): tw is the forward table.
+  // unscaled inverse (the caller folds N^-1 into the key), tw the forward table (mirrored reads)
   template <int XB>
-  __device__ static __forceinline__ void inv3m(double (&x)[E], double *lds, const double *tw, int tid) {
-    static_assert(cross_wave_exchanges() == 1, "three-buffer scheme written for one cross-wave exchange");
+  __device__ static __forceinline__ void inv(double (&x)[E], double *lds, const double *tw, int tid) {
     int since_red = 0;
-    inv3_from<NPASS - 1, XB, true>(x, lds, tw, tid, since_red);
-  }
-  // Single-transform API.
-  __device__ static __forceinline__ void fwd(double (&x)[E], double *lds, const double *tw, int tid) {
-    fwdC<1>(reinterpret_cast<double(&)[1][E]>(x), lds, tw, tid);
-  }
-  __device__ static __forceinline__ void inv(double (&x)[E], double *lds, const double *itw, int tid) {
-    invC<1>(reinterpret_cast<double(&)[1][E]>(x), lds, itw, tid);
+    inv_stages<3, 9, 11>(x, tw, tid, since_red);
+    swap23(x);
+    inv_stages<2, 6, 9>(x, tw, tid, since_red);
+    exchange_w<2, 1>(x, lds, tid);
+    inv_stages<1, 3, 6>(x, tw, tid, since_red);
+    exchange_x<1, 0, XB>(x, lds, tid);
+    inv_stages<0, 0, 3>(x, tw, tid, since_red);
   }
 };
 

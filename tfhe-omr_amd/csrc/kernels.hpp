@@ -18,6 +18,7 @@ constexpr size_t OMR_DEFAULT_BATCH = 16384;  // messages per detect chunk (scrat
 
 struct DeviceTables {
   const double *tw1, *itw1, *tw2, *itw2;  // psi^brv(k), psi^-brv(k) (centred)
+  const double *tw2c;                     // tw2 with stages 9, 10 permuted for CmuxNtt
   const double *lut1, *lut2;              // LUTs, coefficient domain (centred)
   const uint16_t *trace_perm;             // [11][2048] NTT-domain permutation of sigma_g
   const uint16_t *trace_src;              // [11][2048] coefficient source index of sigma_g (+N: negate)

@@ -173,9 +173,9 @@ __global__ __launch_bounds__(BR2L_T, 1) void br2l_kernel(const uint32_t *__restr
                                                          uint64_t *__restrict__ out) {
   using M = Mod<2>;
   constexpr int T = BR2_T, E = BR2_E, N = N2;
-  using NTT = WgNtt<M, T, E>;
+  using NTT = CmuxNtt;
   using DG = Digits2;
-  __shared__ double xbuf[2][NTT::LDS3_DOUBLES];
+  __shared__ double xbuf[2][NTT::LDS_DOUBLES];
   __shared__ double part[2][N];
   __shared__ double tws[N + 136 * 5];  // forward twiddles + the five small-digit stage tables
   const int g = threadIdx.x / T, t = threadIdx.x % T;
@@ -188,7 +188,7 @@ __global__ __launch_bounds__(BR2L_T, 1) void br2l_kernel(const uint32_t *__restr
     const int rr = (2 * N - (b % (2 * N))) % (2 * N);
 #pragma unroll
     for (int e = 0; e < E; ++e) acc[e] = g == 1 ? canon_small<M>(rot_read<N>(tb.lut2, t + e * T, rr)) : 0.0;
-    for (int j = threadIdx.x; j < N; j += BR2L_T) tws[j] = tb.tw2[j];
+    for (int j = threadIdx.x; j < N; j += BR2L_T) tws[j] = tb.tw2c[j];
     if (threadIdx.x <= 128) {  // table k: d * c_k, d = tid - 64 (c = tw1, tw2, tw1 tw2, tw3, tw1 tw3)
       const double w1 = tb.tw2[1], w2 = tb.tw2[2], w3 = tb.tw2[3];
       const double c[5] = {w1, w2, canon<M>(mm<M>(w1, w2)), w3, canon<M>(mm<M>(w1, w3))};
@@ -229,9 +229,9 @@ __global__ __launch_bounds__(BR2L_T, 1) void br2l_kernel(const uint32_t *__restr
 #pragma unroll
         for (int e = 0; e < E; ++e) d[e] = DG::get_int(pk[e], k);
         if (h == 0)  // digits on X0, X1, X0, ...
-          NTT::template fwd3_small<0>(d, t0, x, X, tw, t);
+          NTT::template fwd_small<0>(d, t0, x, X, tw, t);
         else
-          NTT::template fwd3_small<1>(d, t0, x, X, tw, t);
+          NTT::template fwd_small<1>(d, t0, x, X, tw, t);
 #pragma unroll
         for (int e = 0; e < E; ++e) {
           accA[e] += mm<M>(x[e], cur.a[e]);
@@ -254,7 +254,7 @@ __global__ __launch_bounds__(BR2L_T, 1) void br2l_kernel(const uint32_t *__restr
     double s[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) s[e] = red<M>(red<M>(g == 0 ? accA[e] : accB[e]) + part[g][t * E + e]);
-    NTT::template inv3m<0>(s, X, tw, t);
+    NTT::template inv<0>(s, X, tw, t);
 #pragma unroll
     for (int e = 0; e < E; ++e) acc[e] = canon<M>(acc[e] + s[e]);
   }
