@@ -71,39 +71,49 @@ std::vector<double> negacyclic_lut(const std::vector<uint64_t> &v, int N, int lo
   return lut;
 }
 
-// FFT twiddles of WgFft<T, E, L> (device_fft.hpp): node i of stage s -> w^(eps(s, i) / 2),
-// w = exp(i pi / 2n), n = 2^L, eps(0, 0) = n, eps(s+1, 2i) = eps(s, i) / 2,
-// eps(s+1, 2i+1) = eps(s, i) / 2 + 2n (mod 4n). Radix-8 pass p, block hi: A = node (3p, hi),
-// B = node (3p + 1, 2 hi), C = node (3p + 2, 4 hi); entry t * 8^p - 1 + hi holds T_t of
-// (1, C, B, BC, A, AC, AB, ABC), each an exact angle (sum of the nodes' integer half-eps)
-// evaluated in long double and rounded once.
-std::vector<double2> fft_twiddles(int T, int E, int L) {
-  (void)T;
-  const int n = 1 << L, R = __builtin_ctz(E);
+// FFT twiddles of Fft512 (device_fft.hpp, WgFft): node i of stage s -> w^(eps(s, i) / 2),
+// w = exp(i pi / 2n), n = 512, eps(0, 0) = n, eps(s+1, 2i) = eps(s, i) / 2,
+// eps(s+1, 2i+1) = eps(s, i) / 2 + 2n (mod 4n). Layout (WgFft): [0, 7) T_1..T_7 of the pass-0
+// radix-8 block (A = node(0, 0), B = node(1, 0), C = node(2, 0), T = (C, B, BC, A, AC, AB, ABC));
+// 7 + 3 blk + (B, A, AB) of the pass-1 radix-4 block blk (A = node(3, blk), B = node(4, 2 blk));
+// 31 + (t - 1) 32 + hi the pass-2 radix-8 blocks (A = node(5, hi), B = node(6, 2 hi),
+// C = node(7, 4 hi)); 255 + 64 e1 + lane the pass-3 (stage 8) even-sibling node
+// ((lane & 31) << 3 | (lane >> 5) << 2 | e1 << 1). Each entry is an exact angle (sum of the nodes'
+// integer half-eps) evaluated in long double and rounded once.
+std::vector<double2> fft_twiddles() {
+  const int L = 9, n = 1 << L;
   std::vector<double2> tw(n, make_double2(1.0, 0.0));
-  std::vector<std::vector<int>> half(L);  // half[s][i] = eps(s, i) / 2
-  std::vector<int> eps{n};
+  std::vector<std::vector<long>> half(L);  // half[s][i] = eps(s, i) / 2
+  std::vector<long> eps{n};
   for (int s = 0; s < L; ++s) {
-    std::vector<int> next;
-    for (int e : eps) {
+    std::vector<long> next;
+    for (long e : eps) {
       half[s].push_back(e / 2);
       next.push_back((e / 2) % (4 * n));
       next.push_back((e / 2 + 2 * n) % (4 * n));
     }
     eps.swap(next);
   }
-  for (int p = 0; p * R < L; ++p) {
-    const int s0 = p * R, blocks = 1 << s0;
-    for (int hi = 0; hi < blocks; ++hi) {
-      const long a = half[s0][hi], b = half[s0 + 1][2 * hi], c = half[s0 + 2][4 * hi];
-      const long h[8] = {0, c, b, b + c, a, a + c, a + b, a + b + c};
-      for (int t = 1; t < 8; ++t) {
-        const long double ang =
-            3.14159265358979323846264338327950288L * (long double)(h[t] % (8 * n)) / (long double)(2 * n);
-        tw[t * blocks - 1 + hi] = make_double2((double)cosl(ang), (double)sinl(ang));
-      }
-    }
+  auto at = [&](long h) {
+    const long double ang = 3.14159265358979323846264338327950288L * (long double)(h % (8 * n)) / (long double)(2 * n);
+    return make_double2((double)cosl(ang), (double)sinl(ang));
+  };
+  auto radix8 = [&](int s0, int hi, auto put) {
+    const long a = half[s0][hi], b = half[s0 + 1][2 * hi], c = half[s0 + 2][4 * hi];
+    const long h[8] = {0, c, b, b + c, a, a + c, a + b, a + b + c};
+    for (int t = 1; t < 8; ++t) put(t, at(h[t]));
+  };
+  radix8(0, 0, [&](int t, double2 v) { tw[t - 1] = v; });
+  for (int blk = 0; blk < 8; ++blk) {
+    const long a = half[3][blk], b = half[4][2 * blk];
+    tw[7 + 3 * blk] = at(b);
+    tw[7 + 3 * blk + 1] = at(a);
+    tw[7 + 3 * blk + 2] = at(a + b);
   }
+  for (int hi = 0; hi < 32; ++hi) radix8(5, hi, [&](int t, double2 v) { tw[31 + (t - 1) * 32 + hi] = v; });
+  for (int e1 = 0; e1 < 2; ++e1)
+    for (int lane = 0; lane < 64; ++lane)
+      tw[255 + 64 * e1 + lane] = at(half[8][((lane & 31) << 3) | ((lane >> 5) << 2) | (e1 << 1)]);
   return tw;
 }
 
@@ -403,7 +413,7 @@ extern "C" omr_status omr_ctx_create(const omr_detection_key_view *key, int devi
   c->tb.tw2c = c->tables + 3 * N1 + 3 * N2;
   c->tb.trace_src = c->trace_tabs;
   c->tb.trace_perm = c->trace_tabs + TRACE_STEPS * N2;
-  const auto ftw = fft_twiddles(Fft512::T, Fft512::E, Fft512::L);
+  const auto ftw = fft_twiddles();
   if (hipMalloc(&c->fft1, ftw.size() * sizeof(double2)) != hipSuccess)
     return fail(set_error(OMR_ERR_OUT_OF_MEMORY, "omr_ctx_create: tables"));
   if (hipMemcpy(c->fft1, ftw.data(), ftw.size() * sizeof(double2), hipMemcpyHostToDevice) != hipSuccess)

@@ -15,11 +15,9 @@
 // Node i of stage s uses w^(eps(s, i) / 2), eps(0, 0) = n, eps(s+1, 2i) = eps(s, i) / 2,
 // eps(s+1, 2i+1) = eps(s, i) / 2 + 2n (mod 4n). Passes are radix-8 blocks of that tree (WgFft::fwd_pass).
 //
-// T lanes hold E complex values each (N = T E), log2(E) = 3 stages per pass, an LDS exchange
-// between passes (XOR swizzle found by tools/fft_lds_banks.py: no bank conflicts for
-// ds_write_b128 / ds_read_b128), C independent transforms interleaved. One wave per transform.
-//   forward: in  x[e] = coefficient (lane + T e)    out x[e] = transform index (E lane + e)
-//   inverse: in  x[e] = transform index (E lane + e) out x[e] = coefficient (lane + T e)
+// One wave per transform, C independent transforms interleaved (layouts in WgFft below).
+//   forward: in  x[e] = coefficient (lane + 64 e)   out x[e] = transform index jidx(3, lane, e)
+//   inverse: the reverse (keys are transformed by the same forward, so the pointwise products line up)
 #pragma once
 
 #include <utility>
@@ -40,63 +38,80 @@ __device__ __forceinline__ void wave_lds_fence() {
   __builtin_amdgcn_wave_barrier();
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
 }
-// XOR swizzle of the LDS exchange slots, slot(j) = j ^ f(j), f linear over GF(2): no bank
-// conflicts for any exchange of the geometry (tools/fft_lds_banks.py 64 8 9).
-template <int T, int E, int L>
-struct FftSwizzle;
-template <>
-struct FftSwizzle<64, 8, 9> {
-  static constexpr int M[6] = {4, 9, 15, 14, 0, 8};
-};
-
+// Level-1 transform: 512 complex points, one wave (64 lanes x 8 registers), index bits j8..j0
+// (stage s splits on bit 8 - s). Four passes of 3, 2, 3 and 1 stages; jidx(p, lane, e) is the
+// index register e of `lane` holds in pass p:
+//   P0: e -> j8 j7 j6, lane -> j5..j0                                  (coefficient layout lane + 64 e)
+//   P1: e2 -> j5, e1 -> j4, e0 -> j6; lane 5, 4 -> j8, j7, lane 3..0 -> j3..j0
+//       (P0 -> P1: register bits 2, 1 <-> lane bits 5, 4 by v_permlane32/16_swap, no LDS)
+//   P2: e -> j3 j2 j1, lane 5 -> j0, lane 4..0 -> j8..j4                (the one LDS exchange)
+//   P3: e2 -> j0, e1 -> j2, e0 -> j1; lane 5 -> j3, lane 4..0 -> j8..j4
+//       (P2 -> P3: register bit 2 <-> lane bit 5, permlane)
+// P0 and P2 are radix-8 blocks of the twiddle tree: the block's stage-s0 node (hi) has twiddle A,
+// its children B, i B and grandchildren C, i C, w8 C, i w8 C (w8 = exp(i pi / 4)); three radix-2
+// stages equal "x_e *= T_e, then a constant 8-point network" with T = (1, C, B, BC, A, AC, AB, ABC):
+// 80 FP64 operations instead of 96 (the factors i free, w8 folded into FMAs). P1 is two radix-4
+// blocks (register bit 0 = j6 selects the block): T = (1, B, A, AB) on registers (e0, e0 + 2,
+// e0 + 4, e0 + 6), 3 products + 8 additions. P3 is one radix-2 stage, odd siblings (register bit
+// 0 = j1) taking i w. tools/fft_exactness.py (Fft8P) models this structure against the exact
+// negacyclic product. The exchange replaced by the permlane relayouts cost 14 % of the level-1
+// kernel (timing ablation).
+// Twiddle table (double2): [0, 7) T_1..T_7 of P0 (wave-uniform); 7 + 3 blk + (B, A, AB) of P1's
+// block blk = (j8 j7 j6); 31 + (t - 1) 32 + hi, hi = j8..j4 = lane & 31, for P2; 255 + 64 e1 + lane
+// for P3's stage-8 twiddle of the even sibling.
 template <int T_, int E_, int L_>
 struct WgFft {
-  static constexpr int T = T_, E = E_, L = L_, N = T * E, R = ilog2(E), NPASS = (L + R - 1) / R;
-  static_assert(N == (1 << L), "FFT geometry");
-  static_assert(T == 64, "one transform per wave (wave-level LDS synchronisation)");
-  // stages in pass p (the last pass may be shorter)
-  static constexpr int stages(int p) { return (L - p * R) < R ? (L - p * R) : R; }
-
-  // element index of register e in pass p (the WgNtt scheme, partial last pass included)
-  __device__ static __forceinline__ int index(int p, int lane, int e) {
-    const int s0 = p * R, r = stages(p), lb = L - s0 - r;
-    const int F = (lane << (R - r)) | (e >> r);
-    return ((F >> lb) << (L - s0)) | ((e & ((1 << r) - 1)) << lb) | (F & ((1 << lb) - 1));
-  }
-  // bank-conflict-free XOR swizzle (linear over GF(2); folds to constants per unrolled e)
-  template <int... B>
-  __device__ static __forceinline__ int swz_bits(int j, std::integer_sequence<int, B...>) {
-    return (0 ^ ... ^ (((j >> (3 + B)) & 1) * FftSwizzle<T, E, L>::M[B]));
-  }
-  __device__ static __forceinline__ int swz(int j) {
-    return j ^ swz_bits(j, std::make_integer_sequence<int, L - 3>{});
-  }
+  static constexpr int T = T_, E = E_, L = L_, N = T * E;
+  static_assert(T == 64 && E == 8 && L == 9, "written for the level-1 geometry: one wave, 64 x 8");
   static constexpr int BUF = N;  // LDS slots (double2) per transform
-  // slot of register e of `lane` in pass p
-  __device__ static __forceinline__ int slot(int p, int lane, int e) { return swz(index(p, lane, e)); }
-  // Radix-8 passes. Pass P of a lane works on one block of the twiddle tree: the stage-s0 node
-  // hi = F >> lb with twiddle A, its children (B, i B) and grandchildren (C, i C, w8 C, i w8 C),
-  // w8 = exp(i pi / 4) (node 4 hi + 2 is the even child of node 2 hi + 1: eps / 4 + n). Three radix-2
-  // stages on registers e (pairs (e, e + 4) with A; (e, e + 2) with B / i B; (e, e + 1) with C, i C,
-  // w8 C, i w8 C) equal "multiply x_e by T_e, then a constant 8-point network" with
-  // T = (1, C, B, BC, A, AC, AB, ABC): 7 complex products + 24 complex additions, the factors i
-  // free and w8 folded into FMAs -- 80 FP64 operations instead of 96
-  // (tools/fft_exactness.py checks both forms against the exact product).
-  // Table: entry t * 8^P - 1 + hi holds T_t of block hi of pass P (t = 1..7; 511 entries), so a
-  // pass-2 read is lane-contiguous and pass-0 reads are wave-uniform.
-  static_assert(R == 3 && L % R == 0, "radix-8 passes: every pass has three stages");
-  __device__ static __forceinline__ constexpr int tw_base(int p) { return (1 << (3 * p)) - 1; }
-  template <int P>
-  __device__ static __forceinline__ int block_of(int lane) { return lane >> (L - P * R - R); }
-  template <int P, bool G>
-  __device__ static __forceinline__ double2 block_twiddle(const double2 *tws, const double2 *__restrict__ gtw,
-                                                          int t, int hi) {
-    const int idx = t * (1 << (3 * P)) - 1 + hi;
-    if constexpr (P == 0 && G) return gtw[idx];  // hi == 0: uniform, scalar loads
-    return tws[idx];
+
+  __device__ static __forceinline__ int jidx(int p, int lane, int e) {
+    const int l5 = (lane >> 5) & 1, l4 = (lane >> 4) & 1;
+    if (p == 0) return (e << 6) | lane;
+    if (p == 1) return (l5 << 8) | (l4 << 7) | ((e & 1) << 6) | (((e >> 2) & 1) << 5) | (((e >> 1) & 1) << 4) | (lane & 15);
+    if (p == 2) return ((lane & 31) << 4) | (e << 1) | l5;
+    return ((lane & 31) << 4) | (l5 << 3) | (((e >> 1) & 1) << 2) | ((e & 1) << 1) | ((e >> 2) & 1);
+  }
+  // bank-conflict-free XOR swizzle of the P1 <-> P2 exchange: j4, j5, j6, j8 into slot bits 0..3
+  // (ds_write_b128 8-lane groups and ds_read_b128 16-lane groups, both directions; tests/test_fft1_layout.py)
+  __device__ static __forceinline__ int slot(int j) {
+    return j ^ ((j >> 4) & 1) ^ (((j >> 5) & 1) << 1) ^ (((j >> 6) & 1) << 2) ^ (((j >> 8) & 1) << 3);
   }
 
-  // Exchange between passes PF and PT through the wave's LDS buffer (C transforms).
+  // P0 <-> P1 and P2 <-> P3 relayouts (involutions)
+  template <int C>
+  __device__ static __forceinline__ void swap01(double (&xr)[C][E], double (&xi)[C][E]) {
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        if (!(e & 4)) {
+          swap_lane_bit<5>(xr[c][e], xr[c][e + 4]);
+          swap_lane_bit<5>(xi[c][e], xi[c][e + 4]);
+        }
+      }
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        if (!(e & 2)) {
+          swap_lane_bit<4>(xr[c][e], xr[c][e + 2]);
+          swap_lane_bit<4>(xi[c][e], xi[c][e + 2]);
+        }
+      }
+  }
+  template <int C>
+  __device__ static __forceinline__ void swap23(double (&xr)[C][E], double (&xi)[C][E]) {
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        swap_lane_bit<5>(xr[c][e], xr[c][e + 4]);
+        swap_lane_bit<5>(xi[c][e], xi[c][e + 4]);
+      }
+  }
+
+  // P1 <-> P2 through the wave's LDS buffer (C transforms)
   template <int C, int PF, int PT>
   __device__ static __forceinline__ void exchange(double (&xr)[C][E], double (&xi)[C][E],
                                                   double2 *lds, int lane) {
@@ -104,13 +119,13 @@ struct WgFft {
     for (int c = 0; c < C; ++c)
 #pragma unroll
       for (int e = 0; e < E; ++e)
-        lds[c * BUF + slot(PF, lane, e)] = make_double2(xr[c][e], xi[c][e]);
+        lds[c * BUF + slot(jidx(PF, lane, e))] = make_double2(xr[c][e], xi[c][e]);
     wave_lds_sync();
 #pragma unroll
     for (int c = 0; c < C; ++c)
 #pragma unroll
       for (int e = 0; e < E; ++e) {
-        const double2 v = lds[c * BUF + slot(PT, lane, e)];
+        const double2 v = lds[c * BUF + slot(jidx(PT, lane, e))];
         xr[c][e] = v.x;
         xi[c][e] = v.y;
       }
@@ -121,14 +136,21 @@ struct WgFft {
 
   static constexpr double S8 = 0.70710678118654752440;  // 1 / sqrt(2), w8 = S8 (1 + i)
 
+  // radix-8 block twiddle T_t (t = 1..7) of pass P in {0, 2}; pass 0 from the global table with
+  // wave-uniform (scalar) loads when G
+  template <int P, bool G>
+  __device__ static __forceinline__ double2 tw8(const double2 *tws, const double2 *__restrict__ gtw, int t,
+                                                int lane) {
+    if constexpr (P == 0) return G ? gtw[t - 1] : tws[t - 1];
+    return tws[31 + (t - 1) * 32 + (lane & 31)];
+  }
+
   template <int P, int C, bool G = false>
-  __device__ static __forceinline__ void fwd_pass(double (&xr)[C][E], double (&xi)[C][E],
-                                                  const double2 *tws, int lane,
-                                                  const double2 *__restrict__ gtw = nullptr) {
-    const int hi = block_of<P>(lane);
+  __device__ static __forceinline__ void fwd8(double (&xr)[C][E], double (&xi)[C][E], const double2 *tws,
+                                              int lane, const double2 *__restrict__ gtw = nullptr) {
 #pragma unroll
     for (int t = 1; t < 8; ++t) {  // x_t *= T_t
-      const double2 w = block_twiddle<P, G>(tws, gtw, t, hi);
+      const double2 w = tw8<P, G>(tws, gtw, t, lane);
 #pragma unroll
       for (int c = 0; c < C; ++c) {
         const double r = __fma_rn(xr[c][t], w.x, -xi[c][t] * w.y);
@@ -172,12 +194,10 @@ struct WgFft {
       xi[c][7] = __fma_rn(-S8, v3, d2i);
     }
   }
-  // Unscaled inverse of fwd_pass (8 x its inverse): the adjoint network, then x_e *= conj(T_e).
+  // unscaled inverse of fwd8 (8 x its inverse): the adjoint network, then x_e *= conj(T_e)
   template <int P, int C, bool G = false>
-  __device__ static __forceinline__ void inv_pass(double (&xr)[C][E], double (&xi)[C][E],
-                                                  const double2 *tws, int lane,
-                                                  const double2 *__restrict__ gtw = nullptr) {
-    const int hi = block_of<P>(lane);
+  __device__ static __forceinline__ void inv8(double (&xr)[C][E], double (&xi)[C][E], const double2 *tws,
+                                              int lane, const double2 *__restrict__ gtw = nullptr) {
 #pragma unroll
     for (int c = 0; c < C; ++c) {
       const double *o_r = xr[c], *o_i = xi[c];
@@ -215,7 +235,7 @@ struct WgFft {
     }
 #pragma unroll
     for (int t = 1; t < 8; ++t) {  // x_t *= conj(T_t)
-      const double2 w = block_twiddle<P, G>(tws, gtw, t, hi);
+      const double2 w = tw8<P, G>(tws, gtw, t, lane);
 #pragma unroll
       for (int c = 0; c < C; ++c) {
         const double r = __fma_rn(xr[c][t], w.x, xi[c][t] * w.y);
@@ -225,43 +245,126 @@ struct WgFft {
       }
     }
   }
+
+  // P1: two radix-4 blocks
+  __device__ static __forceinline__ int tw4_index(int lane, int e0, int k) {  // k: 0 B, 1 A, 2 AB
+    return 7 + 3 * ((((lane >> 4) & 3) << 1) | e0) + k;
+  }
+  template <int C>
+  __device__ static __forceinline__ void fwd4(double (&xr)[C][E], double (&xi)[C][E], const double2 *tws, int lane) {
+#pragma unroll
+    for (int e0 = 0; e0 < 2; ++e0) {
+      const double2 B = tws[tw4_index(lane, e0, 0)], A = tws[tw4_index(lane, e0, 1)], AB = tws[tw4_index(lane, e0, 2)];
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        const int r0 = e0, r1 = e0 | 2, r2 = e0 | 4, r3 = e0 | 6;
+        const double p1r = __fma_rn(xr[c][r1], B.x, -xi[c][r1] * B.y), p1i = __fma_rn(xr[c][r1], B.y, xi[c][r1] * B.x);
+        const double p2r = __fma_rn(xr[c][r2], A.x, -xi[c][r2] * A.y), p2i = __fma_rn(xr[c][r2], A.y, xi[c][r2] * A.x);
+        const double p3r = __fma_rn(xr[c][r3], AB.x, -xi[c][r3] * AB.y), p3i = __fma_rn(xr[c][r3], AB.y, xi[c][r3] * AB.x);
+        const double a0r = xr[c][r0] + p2r, a0i = xi[c][r0] + p2i, b0r = xr[c][r0] - p2r, b0i = xi[c][r0] - p2i;
+        const double a1r = p1r + p3r, a1i = p1i + p3i, b1r = p1r - p3r, b1i = p1i - p3i;
+        xr[c][r0] = a0r + a1r;
+        xi[c][r0] = a0i + a1i;
+        xr[c][r1] = a0r - a1r;
+        xi[c][r1] = a0i - a1i;
+        xr[c][r2] = b0r - b1i;  // b0 + i b1
+        xi[c][r2] = b0i + b1r;
+        xr[c][r3] = b0r + b1i;  // b0 - i b1
+        xi[c][r3] = b0i - b1r;
+      }
+    }
+  }
+  template <int C>
+  __device__ static __forceinline__ void inv4(double (&xr)[C][E], double (&xi)[C][E], const double2 *tws, int lane) {
+#pragma unroll
+    for (int e0 = 0; e0 < 2; ++e0) {
+      const double2 B = tws[tw4_index(lane, e0, 0)], A = tws[tw4_index(lane, e0, 1)], AB = tws[tw4_index(lane, e0, 2)];
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        const int r0 = e0, r1 = e0 | 2, r2 = e0 | 4, r3 = e0 | 6;
+        const double sr = xr[c][r0] + xr[c][r1], si = xi[c][r0] + xi[c][r1];
+        const double tr = xr[c][r0] - xr[c][r1], ti = xi[c][r0] - xi[c][r1];
+        const double ur = xr[c][r2] + xr[c][r3], ui = xi[c][r2] + xi[c][r3];
+        const double vr = xi[c][r2] - xi[c][r3], vi = xr[c][r3] - xr[c][r2];  // -i (o2 - o3)
+        const double p1r = tr + vr, p1i = ti + vi, p2r = sr - ur, p2i = si - ui, p3r = tr - vr, p3i = ti - vi;
+        xr[c][r0] = sr + ur;
+        xi[c][r0] = si + ui;
+        xr[c][r1] = __fma_rn(p1r, B.x, p1i * B.y);  // * conj(B)
+        xi[c][r1] = __fma_rn(p1i, B.x, -p1r * B.y);
+        xr[c][r2] = __fma_rn(p2r, A.x, p2i * A.y);
+        xi[c][r2] = __fma_rn(p2i, A.x, -p2r * A.y);
+        xr[c][r3] = __fma_rn(p3r, AB.x, p3i * AB.y);
+        xi[c][r3] = __fma_rn(p3i, AB.x, -p3r * AB.y);
+      }
+    }
+  }
+
+  // P3: stage 8, pairs (e, e + 4); register bit 1 selects the even-sibling twiddle, bit 0 the factor i
+  template <int C>
+  __device__ static __forceinline__ void fwd2(double (&xr)[C][E], double (&xi)[C][E], const double2 *tws, int lane) {
+    const double2 W[2] = {tws[255 + lane], tws[255 + 64 + lane]};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const double2 w = W[(e >> 1) & 1];
+      const bool odd = e & 1;
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        const double vr = __fma_rn(xr[c][e + 4], w.x, -xi[c][e + 4] * w.y);
+        const double vi = __fma_rn(xr[c][e + 4], w.y, xi[c][e + 4] * w.x);
+        const double ur = xr[c][e], ui = xi[c][e];
+        xr[c][e] = odd ? ur - vi : ur + vr;  // u + i v  |  u + v
+        xi[c][e] = odd ? ui + vr : ui + vi;
+        xr[c][e + 4] = odd ? ur + vi : ur - vr;
+        xi[c][e + 4] = odd ? ui - vr : ui - vi;
+      }
+    }
+  }
+  template <int C>
+  __device__ static __forceinline__ void inv2(double (&xr)[C][E], double (&xi)[C][E], const double2 *tws, int lane) {
+    const double2 W[2] = {tws[255 + lane], tws[255 + 64 + lane]};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const double2 w = W[(e >> 1) & 1];
+      const bool odd = e & 1;
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        const double ur = xr[c][e], ui = xi[c][e];
+        const double dr = ur - xr[c][e + 4], di = ui - xi[c][e + 4];
+        xr[c][e] = ur + xr[c][e + 4];
+        xi[c][e] = ui + xi[c][e + 4];
+        // (dr + i di) * conj(w); odd node: conj(i w) = -i conj(w)
+        const double tr = __fma_rn(dr, w.x, di * w.y), ti = __fma_rn(di, w.x, -dr * w.y);
+        xr[c][e + 4] = odd ? ti : tr;
+        xi[c][e + 4] = odd ? -tr : ti;
+      }
+    }
+  }
+
   // C transforms at once (lds holds C * BUF complex)
   // G: pass-0 twiddles from the global table gtw (must be non-null)
   template <int C, bool G = false>
   __device__ static __forceinline__ void fwd(double (&xr)[C][E], double (&xi)[C][E], double2 *lds,
                                              const double2 *tws, int lane,
                                              const double2 *__restrict__ gtw = nullptr) {
-    static_assert(NPASS <= 5, "unrolled for up to 5 passes");
-    fwd_pass<0, C, G>(xr, xi, tws, lane, gtw);
-#define OMR_FFT_FWD_STEP(P)                                                                   \
-  if constexpr (NPASS > P) {                                                                  \
-    constexpr int Q = NPASS > P ? P : 1;                                                      \
-    exchange<C, Q - 1, Q>(xr, xi, lds, lane);                                                 \
-    fwd_pass<(NPASS > P ? P : 0), C>(xr, xi, tws, lane);                                      \
-  }
-    OMR_FFT_FWD_STEP(1)
-    OMR_FFT_FWD_STEP(2)
-    OMR_FFT_FWD_STEP(3)
-    OMR_FFT_FWD_STEP(4)
-#undef OMR_FFT_FWD_STEP
+    fwd8<0, C, G>(xr, xi, tws, lane, gtw);
+    swap01<C>(xr, xi);
+    fwd4<C>(xr, xi, tws, lane);
+    exchange<C, 1, 2>(xr, xi, lds, lane);
+    fwd8<2, C>(xr, xi, tws, lane);
+    swap23<C>(xr, xi);
+    fwd2<C>(xr, xi, tws, lane);
   }
   template <int C, bool G = false>
   __device__ static __forceinline__ void inv(double (&xr)[C][E], double (&xi)[C][E], double2 *lds,
                                              const double2 *tws, int lane,
                                              const double2 *__restrict__ gtw = nullptr) {
-    static_assert(NPASS <= 5, "unrolled for up to 5 passes");
-#define OMR_FFT_INV_STEP(P)                                                                   \
-  if constexpr (NPASS > P) {                                                                  \
-    constexpr int Q = NPASS > P ? P : 1;                                                      \
-    inv_pass<(NPASS > P ? P : 0), C>(xr, xi, tws, lane);                                      \
-    exchange<C, Q, Q - 1>(xr, xi, lds, lane);                                                 \
-  }
-    OMR_FFT_INV_STEP(4)
-    OMR_FFT_INV_STEP(3)
-    OMR_FFT_INV_STEP(2)
-    OMR_FFT_INV_STEP(1)
-#undef OMR_FFT_INV_STEP
-    inv_pass<0, C, G>(xr, xi, tws, lane, gtw);
+    inv2<C>(xr, xi, tws, lane);
+    swap23<C>(xr, xi);
+    inv8<2, C>(xr, xi, tws, lane);
+    exchange<C, 2, 1>(xr, xi, lds, lane);
+    inv4<C>(xr, xi, tws, lane);
+    swap01<C>(xr, xi);
+    inv8<0, C, G>(xr, xi, tws, lane, gtw);
   }
   __device__ static __forceinline__ void fwd(double (&xr)[E], double (&xi)[E], double2 *lds,
                                              const double2 *tws, int lane,

@@ -150,6 +150,118 @@ class Fft8(Fft):
         return z
 
 
+class Fft8P(Fft):
+    """The kernel's level-1 transform (WgFft<64, 8, 9>): passes of 3, 2, 3, 1 stages; the relayouts
+    P0 -> P1 and P2 -> P3 are permlane bit swaps (register/lane bits), P1 -> P2 one LDS exchange.
+    jidx(p, e) is the transform index held by register e of each lane in pass p."""
+
+    def __init__(self):
+        super().__init__(64, 8, 9)
+
+    def jidx(self, p, e):
+        l = self.lane
+        b = lambda v, k: (v >> k) & 1
+        if p == 0:
+            return (e << 6) | l
+        if p == 1:
+            return (b(l, 5) << 8) | (b(l, 4) << 7) | (b(e, 0) << 6) | (b(e, 2) << 5) | (b(e, 1) << 4) | (l & 15)
+        if p == 2:
+            return ((l & 31) << 4) | (e << 1) | b(l, 5)
+        return ((l & 31) << 4) | (b(l, 5) << 3) | (b(e, 1) << 2) | (b(e, 0) << 1) | b(e, 2)
+
+    def relayout(self, x, pf, pt):
+        buf = np.full(self.n, np.nan, dtype=np.complex128)
+        for e in range(8):
+            buf[self.jidx(pf, e)] = x[:, e]
+        return np.stack([buf[self.jidx(pt, e)] for e in range(8)], axis=1)
+
+    def blocks(self, p):
+        """per-lane premultiplication twiddles of pass p's blocks"""
+        tw, l = self.tw, self.lane
+        if p in (0, 2):
+            hi = 0 if p == 0 else l & 31
+            s0 = 0 if p == 0 else 5
+            A, B, C = tw[(1 << s0) + hi], tw[(2 << s0) + 2 * hi], tw[(4 << s0) + 4 * hi]
+            return [np.ones(64) * v for v in (1, C, B, B * C, A, A * C, A * B, A * B * C)]
+        if p == 1:  # two radix-4 blocks (register bit 0 = j6): T = (1, B, A, AB) on registers (e0, e0|2, e0|4, e0|6)
+            out = []
+            for e0 in (0, 1):
+                blk = ((l >> 5) << 2) | (((l >> 4) & 1) << 1) | e0
+                A, B = tw[8 + blk], tw[16 + 2 * blk]
+                out.append([np.ones(64), B, A, A * B])
+            return out
+        node = ((l & 31) << 3) | ((l >> 5) << 2)  # stage 8, even node for e1 = 0 (+2 for e1 = 1)
+        return [tw[256 + node], tw[256 + node + 2]]
+
+    @staticmethod
+    def net8(x):
+        P = [x[:, e] for e in range(8)]
+        a = [P[e] + P[e + 4] for e in range(4)]
+        b = [P[e] - P[e + 4] for e in range(4)]
+        c0, c2, c1, c3 = a[0] + a[2], a[0] - a[2], a[1] + a[3], a[1] - a[3]
+        d0, d2, d1, d3 = b[0] + 1j * b[2], b[0] - 1j * b[2], b[1] + 1j * b[3], b[1] - 1j * b[3]
+        w8 = S8 * (1 + 1j)
+        return np.stack([c0 + c1, c0 - c1, c2 + 1j * c3, c2 - 1j * c3, d0 + w8 * d1, d0 - w8 * d1,
+                         d2 + 1j * w8 * d3, d2 - 1j * w8 * d3], axis=1)
+
+    @staticmethod
+    def net8_adj(x):
+        o = [x[:, e] for e in range(8)]
+        c0, c1, c2, c3 = o[0] + o[1], o[0] - o[1], o[2] + o[3], -1j * (o[2] - o[3])
+        d0, d1 = o[4] + o[5], (1 - 1j) * (o[4] - o[5])
+        d2, d3 = o[6] + o[7], (-1 - 1j) * (o[6] - o[7])
+        a0, a2, a1, a3 = c0 + c2, c0 - c2, c1 + c3, c1 - c3
+        b0, b2, b1, b3 = d0 + d2, -1j * (d0 - d2), d1 + d3, -1j * (d1 - d3)
+        return np.stack([a0 + b0, a1 + S8 * b1, a2 + b2, a3 + S8 * b3, a0 - b0, a1 - S8 * b1, a2 - b2,
+                         a3 - S8 * b3], axis=1)
+
+    def fwd(self, z):
+        x = np.stack([z[self.lane + 64 * e] for e in range(8)], axis=1).astype(np.complex128)
+        x = self.net8(x * np.stack(self.blocks(0), axis=1))
+        x = self.relayout(x, 0, 1)
+        for e0, T in zip((0, 1), self.blocks(1)):
+            r = [e0, e0 | 2, e0 | 4, e0 | 6]
+            P = [x[:, r[k]] * T[k] for k in range(4)]
+            a0, a1, b0, b1 = P[0] + P[2], P[1] + P[3], P[0] - P[2], P[1] - P[3]
+            x[:, r[0]], x[:, r[1]], x[:, r[2]], x[:, r[3]] = a0 + a1, a0 - a1, b0 + 1j * b1, b0 - 1j * b1
+        x = self.relayout(x, 1, 2)
+        x = self.net8(x * np.stack(self.blocks(2), axis=1))
+        x = self.relayout(x, 2, 3)
+        W = self.blocks(3)
+        for e in range(4):  # stage 8 pairs (e, e + 4); register bit 0 = j1 odd siblings take i w
+            w = W[(e >> 1) & 1] * (1j if e & 1 else 1)
+            u, v = x[:, e].copy(), x[:, e + 4] * w
+            x[:, e], x[:, e + 4] = u + v, u - v
+        out = np.zeros(self.n, dtype=np.complex128)
+        for e in range(8):
+            out[self.jidx(3, e)] = x[:, e]
+        return out
+
+    def inv(self, X):
+        x = np.stack([X[self.jidx(3, e)] for e in range(8)], axis=1).astype(np.complex128)
+        W = self.blocks(3)
+        for e in range(4):
+            w = W[(e >> 1) & 1] * (1j if e & 1 else 1)
+            u, v = x[:, e].copy(), x[:, e + 4].copy()
+            x[:, e], x[:, e + 4] = u + v, (u - v) * np.conj(w)
+        x = self.relayout(x, 3, 2)
+        x = self.net8_adj(x) * np.conj(np.stack(self.blocks(2), axis=1))
+        x = self.relayout(x, 2, 1)
+        for e0, T in zip((0, 1), self.blocks(1)):
+            r = [e0, e0 | 2, e0 | 4, e0 | 6]
+            o = [x[:, r[k]] for k in range(4)]
+            s_, t_, u_, v_ = o[0] + o[1], o[0] - o[1], o[2] + o[3], -1j * (o[2] - o[3])
+            P = [s_ + u_, t_ + v_, s_ - u_, t_ - v_]
+            for k in range(4):
+                x[:, r[k]] = P[k] * np.conj(T[k])
+        x = self.relayout(x, 1, 0)
+        x = self.net8_adj(x) * np.conj(np.stack(self.blocks(0), axis=1))
+        z = np.zeros(self.n, dtype=np.complex128)
+        for e in range(8):
+            z[self.lane + 64 * e] = x[:, e]
+        return z
+
+
 def fold(p):
     h = len(p) // 2
     return p[:h] + 1j * p[h:]
@@ -179,7 +291,7 @@ def adversarial(keys, dmax, N, rng):
 
 def run(geoms, N, kbits, dmax, rows, trials=4, radix8=False):
     rng = np.random.default_rng(5)
-    ffts = [Fft(*g) for g in geoms] + ([Fft8(*g) for g in geoms] if radix8 else [])
+    ffts = [Fft(*g) for g in geoms] + ([Fft8(*g) for g in geoms] + [Fft8P()] if radix8 else [])
     worst = 0.0
     for trial in range(trials):
         keys = [rng.integers(-(1 << (kbits - 1)), 1 << (kbits - 1), N) for _ in range(rows)]
