@@ -51,27 +51,51 @@ struct Lvl1Int {
   }
 };
 
+// br1f keeps ACC offset by H: ac' = ac + H in [0, Q) (u32). A value y in (-Q, 2Q) is reduced to
+// [0, Q) by one v_min3_u32(y, y + Q, y - Q) (the wrapped operands lose), the digit word of the
+// canonical residue y' - H is ((y' - H + 2^6 + 2^7 DIGIT_BIAS) >> 7) ^ DIGIT_BIAS (the bias folded
+// in before the shift), and the stored negacyclic extension 2H - ac' is again "value + H": 7
+// integer operations per digit word instead of 10, 4 per accumulator update instead of 7.
+struct Lvl1Off {
+  static constexpr uint32_t Q = (uint32_t)Lvl1Int::Q, H = (uint32_t)Lvl1Int::H;
+  __device__ static __forceinline__ uint32_t fold(uint32_t y, uint32_t yq, uint32_t ymq) {  // y, y + Q, y - Q
+    return min(min(y, yq), ymq);
+  }
+  // digit word of canon(x - ac) from x' = x + H (stored) and n = 2H - ac' = H - ac
+  __device__ static __forceinline__ uint32_t digits(uint32_t xs, uint32_t n) {
+    const uint32_t y = fold(xs + n - H, xs + n + (Q - H), xs + n - (Q + H));
+    constexpr uint32_t C = (uint32_t)((1 << (DROP1 - 1)) - Lvl1Int::H + (Lvl1Int::DIGIT_BIAS << DROP1));
+    return (uint32_t)((int)(y + C) >> DROP1) ^ (uint32_t)Lvl1Int::DIGIT_BIAS;
+  }
+  // ac' + r for r in [-H - 1, H + 1], reduced to [0, Q)
+  __device__ static __forceinline__ uint32_t add(uint32_t acp, int r) {
+    const uint32_t s = acp + (uint32_t)r;
+    return fold(s, s + Q, s - Q);
+  }
+};
+
 // ACC layout: ac[p][h * 8 + e] = coefficient lane + 64 e + 512 h of poly p (0 mask, 1 body).
 __device__ __forceinline__ int acc_coef(int lane, int i) { return lane + 64 * (i & 7) + 512 * (i >> 3); }
 
 // digits of (X^a - 1) * ACC for both polys. Each poly is staged with its negacyclic extension
 // ext = [ACC, -ACC] (2N int32 = the wave's 8 KB buffer st), so (X^a * ACC)[j] = ext[(j - a) mod 2N]:
 // one masked index and no sign fix-up per coefficient.
-__device__ __forceinline__ void br1f_digits(const int (&ac)[2][16], int *st, int a, int lane,
+// (ACC in the Lvl1Off representation: ext = [ac', 2H - ac'], every entry "value + H".)
+__device__ __forceinline__ void br1f_digits(const uint32_t (&ac)[2][16], uint32_t *st, int a, int lane,
                                             uint32_t (&pk)[2][16]) {
 #pragma unroll
   for (int p = 0; p < 2; ++p) {
+    uint32_t n[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
+      n[i] = 2 * Lvl1Off::H - ac[p][i];
       st[acc_coef(lane, i)] = ac[p][i];
-      st[N1 + acc_coef(lane, i)] = -ac[p][i];
+      st[N1 + acc_coef(lane, i)] = n[i];
     }
     wave_lds_sync();
     const int base = lane - a + 2 * N1;
 #pragma unroll
-    for (int i = 0; i < 16; ++i)
-      pk[p][i] = Lvl1Int::digits(
-          Lvl1Int::canon(st[(base + acc_coef(0, i)) & (2 * N1 - 1)] - ac[p][i]));
+    for (int i = 0; i < 16; ++i) pk[p][i] = Lvl1Off::digits(st[(base + acc_coef(0, i)) & (2 * N1 - 1)], n[i]);
     wave_lds_fence();  // the next poly's writes stay below these reads
   }
 }
@@ -113,13 +137,13 @@ __device__ __forceinline__ void wg_barrier_lds() {  // LDS reads/writes done, th
 // One CMUX step with LDS-staged key rows. q0 = first global row of this step; rows q0..q0+7 are
 // consumed, the next step's first row is prefetched on the way. xch: the wave's exchange buffer
 // (Fft512::BUF).
-__device__ __forceinline__ void br1f_step_lds(int (&ac)[2][16], double2 *xch, const double2 *tws, int a,
+__device__ __forceinline__ void br1f_step_lds(uint32_t (&ac)[2][16], double2 *xch, const double2 *tws, int a,
                                               const double2 *__restrict__ bskf, int q0, int qtotal,
                                               double2 *kbuf, int lane, int wave,
                                               const double2 *__restrict__ gtw) {
   using F = Fft512;
   uint32_t pk[2][16];
-  br1f_digits(ac, reinterpret_cast<int *>(xch), a, lane, pk);
+  br1f_digits(ac, reinterpret_cast<uint32_t *>(xch), a, lane, pk);
   double outr[2][1][8], outi[2][1][8];
 #pragma unroll
   for (int o = 0; o < 2; ++o)
@@ -162,7 +186,7 @@ __device__ __forceinline__ void br1f_step_lds(int (&ac)[2][16], double2 *xch, co
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const double v = rint(i < 8 ? outr[o][0][i] : outi[o][0][i - 8]);  // exact (< 2^43)
-      ac[o][i] = Lvl1Int::canon(ac[o][i] + (int)red<Mod<1>>(v));
+      ac[o][i] = Lvl1Off::add(ac[o][i], (int)red<Mod<1>>(v));
     }
   }
 }
@@ -200,12 +224,12 @@ __global__ __launch_bounds__(64 * BR1F_WPG, 2) void br1f_kernel(
     b = lwe_b[gi] & (Q0 - 1);
   }
   // ACC = (0, X^{-b} * LUT1)
-  int ac[2][16];
+  uint32_t ac[2][16];  // Lvl1Off: ac + H
   const int r0 = (2 * N1 - (b % (2 * N1))) % (2 * N1);
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
-    ac[0][i] = 0;
-    ac[1][i] = (int)canon_small<Mod<1>>(rot_read<N1>(tb.lut1, acc_coef(lane, i), r0));
+    ac[0][i] = Lvl1Off::H;
+    ac[1][i] = (uint32_t)((int)canon_small<Mod<1>>(rot_read<N1>(tb.lut1, acc_coef(lane, i), r0)) + Lvl1Int::H);
   }
   for (int j = threadIdx.x; j < NF; j += 64 * W) tws[j] = tb.fft1[j];
   __syncthreads();
@@ -222,7 +246,7 @@ __global__ __launch_bounds__(64 * BR1F_WPG, 2) void br1f_kernel(
   if (mode == 0) {  // extract_lwe_locally (coefficient 0), detector.rs:561
     int *st = reinterpret_cast<int *>(xch);
 #pragma unroll
-    for (int i = 0; i < 16; ++i) st[acc_coef(lane, i)] = ac[0][i];
+    for (int i = 0; i < 16; ++i) st[acc_coef(lane, i)] = (int)ac[0][i] - Lvl1Int::H;
     wave_lds_sync();
     uint32_t *o = ext + g * (N1 + 1);
 #pragma unroll
@@ -230,13 +254,13 @@ __global__ __launch_bounds__(64 * BR1F_WPG, 2) void br1f_kernel(
       const int j = acc_coef(lane, i);
       o[j] = Lvl1Int::to_u32(j == 0 ? st[0] : -st[N1 - j]);
     }
-    if (lane == 0) o[N1] = Lvl1Int::to_u32(ac[1][0]);
+    if (lane == 0) o[N1] = Lvl1Int::to_u32((int)ac[1][0] - Lvl1Int::H);
   } else {
     uint64_t *o = rlwe_out + g * 2 * N1;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      o[acc_coef(lane, i)] = Lvl1Int::to_u32(ac[0][i]);
-      o[N1 + acc_coef(lane, i)] = Lvl1Int::to_u32(ac[1][i]);
+      o[acc_coef(lane, i)] = Lvl1Int::to_u32((int)ac[0][i] - Lvl1Int::H);
+      o[N1 + acc_coef(lane, i)] = Lvl1Int::to_u32((int)ac[1][i] - Lvl1Int::H);
     }
   }
 }
