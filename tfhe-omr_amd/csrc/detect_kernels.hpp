@@ -108,7 +108,7 @@ struct KeyRow {
 template <int T, int E, typename KeyT>
 __device__ __forceinline__ void cmux_step3(double (&acc0)[E], double (&acc1)[E], double *xch, int a,
                                            const KeyT *__restrict__ ggsw, const double *tw, int tid,
-                                           const double *t0) {
+                                           const double *t0, const double *__restrict__ gtw) {
   using M = Mod<2>;
   using NTT = CmuxNtt;
   using DG = Digits2;
@@ -144,9 +144,9 @@ __device__ __forceinline__ void cmux_step3(double (&acc0)[E], double (&acc1)[E],
 #pragma unroll
         for (int e = 0; e < E; ++e) d[e] = DG::get_int(pk[e], k);
         if ((h ^ p) == 0)  // mask digits on X0, X1, ...; body digits on X1, X0, ...
-          NTT::template fwd_small<0>(d, t0, x, xch, tw, tid);
+          NTT::template fwd_small<0>(d, t0, x, xch, tw, tid, gtw);
         else
-          NTT::template fwd_small<1>(d, t0, x, xch, tw, tid);
+          NTT::template fwd_small<1>(d, t0, x, xch, tw, tid, gtw);
 #pragma unroll
         for (int e = 0; e < E; ++e) {
           accA[e] += mm<M>(x[e], (double)cur.a[e]);
@@ -170,10 +170,10 @@ __device__ __forceinline__ void cmux_step3(double (&acc0)[E], double (&acc1)[E],
     accA[e] = red<M>(accA[e]);
     accB[e] = red<M>(accB[e]);
   }
-  NTT::template inv<1>(accA, xch, tw, tid);
+  NTT::template inv<1>(accA, xch, tw, tid, gtw);
 #pragma unroll
   for (int e = 0; e < E; ++e) acc0[e] = canon<M>(acc0[e] + accA[e]);
-  NTT::template inv<0>(accB, xch, tw, tid);
+  NTT::template inv<0>(accB, xch, tw, tid, gtw);
 #pragma unroll
   for (int e = 0; e < E; ++e) acc1[e] = canon<M>(acc1[e] + accB[e]);
 }
@@ -331,7 +331,7 @@ __global__ __launch_bounds__(BR2_T, BR2_WAVES) void br2_trace_kernel(const uint3
   for (int i = 0; i < NI; ++i) {
     const int a = (int)__builtin_amdgcn_readfirstlane(lwe[i]) & (2 * N - 1);
     if (a == 0) continue;  // (X^0 - 1) * ACC = 0
-    cmux_step3<T, E, double>(acc0, acc1, xch, a, bsk2 + (size_t)i * (2 * D2 * 2 * N), tw, tid, t0);
+    cmux_step3<T, E, double>(acc0, acc1, xch, a, bsk2 + (size_t)i * (2 * D2 * 2 * N), tw, tid, t0, tb.tw2c);
   }
   uint64_t *o = out + wg * 2 * N;
   if (mode == 1) {

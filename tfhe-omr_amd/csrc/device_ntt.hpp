@@ -345,8 +345,11 @@ struct CmuxNtt {
   // ds_write_b64 / ds_read_b64 in both P1 and P2 layouts (tests/test_cmux_layout.py)
   __device__ static __forceinline__ int padw(int j) { return j ^ (((j >> 5) & 15) << 1) ^ ((j >> 8) & 1); }
 
-  template <int P, int S, bool INV>
-  __device__ static __forceinline__ void stage(double (&x)[E], const double *tw, int tid, int &since_red) {
+  // Pass-0 twiddles (stages 0..2) are wave-uniform: with G they come from the global table gt
+  // (scalar loads, SGPRs) instead of LDS, whose reads the exchange fences would force again.
+  template <int P, int S, bool INV, bool G = false>
+  __device__ static __forceinline__ void stage(double (&x)[E], const double *tw, int tid, int &since_red,
+                                               const double *__restrict__ gt = nullptr) {
     constexpr int h = 1 << rbit(P, L - 1 - S);
     if (since_red >= (INV ? M::RED_INV : M::RED_FWD)) {
 #pragma unroll
@@ -358,12 +361,12 @@ struct CmuxNtt {
       if (e & h) continue;
       const int off = cmux_tw_off(P, S, tid, e);
       if constexpr (!INV) {
-        const double w = tw[(1 << S) + off];
+        const double w = (P == 0 && G) ? gt[(1 << S) + off] : tw[(1 << S) + off];
         const double u = x[e], v = mm<M>(x[e + h], w);
         x[e] = u + v;
         x[e + h] = u - v;
       } else {  // psi^-brv(2^s + j) = -psi^brv(2^(s+1) - 1 - j): the forward table mirrored
-        const double w = tw[(2 << S) - 1 - off];
+        const double w = (P == 0 && G) ? gt[(2 << S) - 1 - off] : tw[(2 << S) - 1 - off];
         const double u = x[e], v = x[e + h];
         x[e] = u + v;
         x[e + h] = mm<M>(v - u, w);
@@ -371,29 +374,34 @@ struct CmuxNtt {
     }
     ++since_red;
   }
-  template <int P, int S0, int S1>
-  __device__ static __forceinline__ void fwd_stages(double (&x)[E], const double *tw, int tid, int &since_red) {
+  template <int P, int S0, int S1, bool G = false>
+  __device__ static __forceinline__ void fwd_stages(double (&x)[E], const double *tw, int tid, int &since_red,
+                                                    const double *__restrict__ gt = nullptr) {
     if constexpr (S0 < S1) {
-      stage<P, S0, false>(x, tw, tid, since_red);
-      fwd_stages<P, S0 + 1, S1>(x, tw, tid, since_red);
+      stage<P, S0, false, G>(x, tw, tid, since_red, gt);
+      fwd_stages<P, S0 + 1, S1, G>(x, tw, tid, since_red, gt);
     }
   }
-  template <int P, int S0, int S1>  // stages S1 - 1 down to S0
-  __device__ static __forceinline__ void inv_stages(double (&x)[E], const double *tw, int tid, int &since_red) {
+  template <int P, int S0, int S1, bool G = false>  // stages S1 - 1 down to S0
+  __device__ static __forceinline__ void inv_stages(double (&x)[E], const double *tw, int tid, int &since_red,
+                                                    const double *__restrict__ gt = nullptr) {
     if constexpr (S0 < S1) {
-      stage<P, S1 - 1, true>(x, tw, tid, since_red);
-      inv_stages<P, S0, S1 - 1>(x, tw, tid, since_red);
+      stage<P, S1 - 1, true, G>(x, tw, tid, since_red, gt);
+      inv_stages<P, S0, S1 - 1, G>(x, tw, tid, since_red, gt);
     }
   }
-  // cross-wave exchange P0 <-> P1 through X0 / X1 (no trailing barrier: see the buffer rule)
+  // cross-wave exchange P0 <-> P1 through X0 / X1 (no trailing barrier: see the buffer rule).
+  // Unswizzled: consecutive lanes hold consecutive indices in both layouts (P0: tid, P1: tid & 31),
+  // so ds_write_b64 16-lane and ds_read_b64 32-lane groups are conflict free, and every address is
+  // a per-thread base plus an immediate offset (256 e and 32 e doubles): two address registers.
   template <int PF, int PT, int XB>
   __device__ static __forceinline__ void exchange_x(double (&x)[E], double *lds, int tid) {
     double *buf = lds + XB * N;
 #pragma unroll
-    for (int e = 0; e < E; ++e) buf[G::pad(cmux_idx(PF, tid, e))] = x[e];
+    for (int e = 0; e < E; ++e) buf[cmux_idx(PF, tid, e)] = x[e];
     __syncthreads();
 #pragma unroll
-    for (int e = 0; e < E; ++e) x[e] = buf[G::pad(cmux_idx(PT, tid, e))];
+    for (int e = 0; e < E; ++e) x[e] = buf[cmux_idx(PT, tid, e)];
     __builtin_amdgcn_wave_barrier();  // keep the next writes below these reads (in-order LDS)
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
   }
@@ -445,7 +453,8 @@ struct CmuxNtt {
   // exact range (replayed in tests/test_fp64_residues.py).
   template <int XB>
   __device__ static __forceinline__ void fwd_small(const int (&d)[E], const double *t0, double (&x)[E],
-                                                   double *lds, const double *tw, int tid) {
+                                                   double *lds, const double *tw, int tid,
+                                                   const double *__restrict__ gt) {
     const double *T1 = t0, *T2 = t0 + 136, *T3 = t0 + 272, *T4 = t0 + 408, *T5 = t0 + 544;
     const double a4 = T1[d[4] + 64], a5 = T1[d[5] + 64];
     const double x0 = (double)d[0] + a4, x4 = (double)d[0] - a4;
@@ -461,12 +470,14 @@ struct CmuxNtt {
     x[5] = x5 + v5;
     x[7] = x5 - v5;
     int since_red = 2;
-    fwd_stages<0, 2, 3>(x, tw, tid, since_red);
+    fwd_stages<0, 2, 3, true>(x, tw, tid, since_red, gt);
     fwd_rest<XB>(x, lds, tw, tid, since_red);
   }
-  // unscaled inverse (the caller folds N^-1 into the key), tw the forward table (mirrored reads)
+  // unscaled inverse (the caller folds N^-1 into the key), tw the forward table (mirrored reads);
+  // gt: the same table in global memory (pass-0 twiddles)
   template <int XB>
-  __device__ static __forceinline__ void inv(double (&x)[E], double *lds, const double *tw, int tid) {
+  __device__ static __forceinline__ void inv(double (&x)[E], double *lds, const double *tw, int tid,
+                                             const double *__restrict__ gt) {
     int since_red = 0;
     inv_stages<3, 9, 11>(x, tw, tid, since_red);
     swap23(x);
@@ -474,7 +485,7 @@ struct CmuxNtt {
     exchange_w<2, 1>(x, lds, tid);
     inv_stages<1, 3, 6>(x, tw, tid, since_red);
     exchange_x<1, 0, XB>(x, lds, tid);
-    inv_stages<0, 0, 3>(x, tw, tid, since_red);
+    inv_stages<0, 0, 3, true>(x, tw, tid, since_red, gt);
   }
 };
 

@@ -229,9 +229,9 @@ __global__ __launch_bounds__(BR2L_T, 1) void br2l_kernel(const uint32_t *__restr
 #pragma unroll
         for (int e = 0; e < E; ++e) d[e] = DG::get_int(pk[e], k);
         if (h == 0)  // digits on X0, X1, X0, ...
-          NTT::template fwd_small<0>(d, t0, x, X, tw, t);
+          NTT::template fwd_small<0>(d, t0, x, X, tw, t, tb.tw2c);
         else
-          NTT::template fwd_small<1>(d, t0, x, X, tw, t);
+          NTT::template fwd_small<1>(d, t0, x, X, tw, t, tb.tw2c);
 #pragma unroll
         for (int e = 0; e < E; ++e) {
           accA[e] += mm<M>(x[e], cur.a[e]);
@@ -254,7 +254,7 @@ __global__ __launch_bounds__(BR2L_T, 1) void br2l_kernel(const uint32_t *__restr
     double s[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) s[e] = red<M>(red<M>(g == 0 ? accA[e] : accB[e]) + part[g][t * E + e]);
-    NTT::template inv<0>(s, X, tw, t);
+    NTT::template inv<0>(s, X, tw, t, tb.tw2c);
 #pragma unroll
     for (int e = 0; e < E; ++e) acc[e] = canon<M>(acc[e] + s[e]);
   }
