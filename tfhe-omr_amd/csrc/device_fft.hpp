@@ -148,9 +148,13 @@ struct WgFft {
   template <int P, int C, bool G = false>
   __device__ static __forceinline__ void fwd8(double (&xr)[C][E], double (&xi)[C][E], const double2 *tws,
                                               int lane, const double2 *__restrict__ gtw = nullptr) {
+    double2 wt[8];  // the block's twiddles, all requested before the first use (one LDS round trip)
+#pragma unroll
+    for (int t = 1; t < 8; ++t) wt[t] = tw8<P, G>(tws, gtw, t, lane);
+    if constexpr (P != 0) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int t = 1; t < 8; ++t) {  // x_t *= T_t
-      const double2 w = tw8<P, G>(tws, gtw, t, lane);
+      const double2 w = wt[t];
 #pragma unroll
       for (int c = 0; c < C; ++c) {
         const double r = __fma_rn(xr[c][t], w.x, -xi[c][t] * w.y);
@@ -233,9 +237,13 @@ struct WgFft {
       xr[c][7] = __fma_rn(-S8, b3r, a3r);
       xi[c][7] = __fma_rn(-S8, b3i, a3i);
     }
+    double2 wt[8];
+#pragma unroll
+    for (int t = 1; t < 8; ++t) wt[t] = tw8<P, G>(tws, gtw, t, lane);
+    if constexpr (P != 0) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int t = 1; t < 8; ++t) {  // x_t *= conj(T_t)
-      const double2 w = tw8<P, G>(tws, gtw, t, lane);
+      const double2 w = wt[t];
 #pragma unroll
       for (int c = 0; c < C; ++c) {
         const double r = __fma_rn(xr[c][t], w.x, xi[c][t] * w.y);
