@@ -52,12 +52,16 @@ def test_level1_closed_form_digits():
 
 def test_level2_closed_form_digits():
     v = _residues(Q2, 500_000, 2)
-    y = np.floor(v.astype(np.float64) / 256 + 0.5) + 17315143744.0  # exact in FP64 (< 2^42)
+    # detect_kernels.hpp Digits2: bias 64 (1 + 128 + ... + 128^5), exact in FP64 (0 <= y' < 2^43)
+    y = np.floor(v.astype(np.float64) / 256 + 0.5) + 2216338399296.0
+    assert y.min() >= 0 and y.max() < 2.0 ** 43
     hi = np.floor(y / 2097152.0)
     lo = (y - hi * 2097152.0).astype(np.int64)
     hi = hi.astype(np.int64)
-    closed = [((lo >> (7 * k)) & 127) - 64 for k in range(3)] + [((hi >> (7 * k)) & 127) - 64 for k in range(2)]
-    closed.append(hi >> 14)
+    assert lo.max() < 1 << 21 and hi.max() < 1 << 22
+    # field j of either word: offset 7 j, width 7 (j < 2) or 8 (j = 2; bit 21 of lo is zero)
+    field = lambda w, j: (w >> (7 * j)) & (255 if j == 2 else 127)
+    closed = [field(lo, j) - 64 for j in range(3)] + [field(hi, j) - 64 for j in range(3)]
     for a, b in zip(_recursive(v, 7, 6, 8), closed):
         assert np.array_equal(a, b)
 

@@ -46,8 +46,7 @@ struct Lvl1Int {
   // shift down). A v_bfe_i32 in inline asm is slower (it constrains the scheduler), and
   // __builtin_amdgcn_sbfe with a run-time width is miscompiled by ROCm 7.2 (v_cvt_f64_u32).
   __device__ static __forceinline__ double digit(uint32_t w, int k) {
-    const int s1 = k < D1 - 1 ? 32 - LOGB1 * (k + 1) : 0, s2 = k < D1 - 1 ? 32 - LOGB1 : LOGB1 * (D1 - 1);
-    return (double)((int)(w << s1) >> s2);
+    return (double)(int)__builtin_amdgcn_sbfe(w, LOGB1 * k, k < D1 - 1 ? LOGB1 : 32 - LOGB1 * (D1 - 1));
   }
 };
 

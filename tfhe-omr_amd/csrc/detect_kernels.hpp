@@ -9,28 +9,31 @@
 namespace omr {
 
 // Level-2 gadget digits (logB 7, d 6, drop 8) in closed form: y = floor((v + 2^7) / 2^8) has
-// balanced base-128 digits d_k in [-64, 63] (k < 5) and a top digit; with the bias
-// 64 (1 + 128 + ... + 128^4), y' = y + bias is exact in FP64 (|y'| < 2^42) and splits exactly into
-// lo = y' mod 2^21 (digits 0-2) and hi = floor(y' / 2^21) (digits 3-4, top = hi >> 14). Same
-// digits as the recursive NonPowOf2ApproxSignedBasis decomposition of the oracle (gadget
-// convention in include/omr_gpu.h; tests/test_digit_forms.py checks every boundary).
+// balanced base-128 digits d_k in [-64, 63] (k < 5) and a top digit d_5 in [-64, 64]; with the
+// bias 64 (1 + 128 + ... + 128^5), y' = y + bias is exact in FP64 (0 <= y' < 2^43) and splits
+// exactly into lo = y' mod 2^21 (fields 0-2) and hi = floor(y' / 2^21) (fields 3-5). Field k holds
+// d_k + 64: 7 bits at 7 (k mod 3) in word k / 3, the top field 8 bits (bit 21 of lo is zero, so
+// the (offset, width) of field j of either word is (7 j, j == 2 ? 8 : 7)). Same digits as the
+// recursive NonPowOf2ApproxSignedBasis decomposition of the oracle (gadget convention in
+// include/omr_gpu.h; tests/test_digit_forms.py checks every boundary).
 struct Digits2 {
   static constexpr int DW = 2;
   static_assert(LOGB2 == 7 && D2 == 6 && DROP2 == 8, "closed form written for the level-2 basis");
   __device__ static __forceinline__ void pack(double v, uint32_t (&pk)[DW]) {
-    const double y = floor(__fma_rn(v, 1.0 / 256.0, 0.5)) + 17315143744.0;
+    const double y = floor(__fma_rn(v, 1.0 / 256.0, 0.5)) + 2216338399296.0;  // + 17315143744 + 64 * 2^35
     const double hi = floor(y * (1.0 / 2097152.0));
     const double lo = __fma_rn(-hi, 2097152.0, y);
     pk[0] = (uint32_t)(int)lo;
     pk[1] = (uint32_t)(int)hi;
   }
-  __device__ static __forceinline__ int get_int(const uint32_t (&pk)[DW], int k) {
-    if (k == D2 - 1) return (int)pk[1] >> 14;
-    const uint32_t w = k < 3 ? pk[0] : pk[1];
-    const int sh = 7 * (k < 3 ? k : k - 3);
-    return (int)((w >> sh) & 127u) - 64;
+  // d_{j + 3 h} + 64 (the word is chosen at compile time, the offset may be a run-time uniform)
+  template <int H>
+  __device__ static __forceinline__ int field(const uint32_t (&pk)[DW], int j) {
+    return (int)__builtin_amdgcn_ubfe(pk[H], 7 * j, j == 2 ? 8 : 7);
   }
-  __device__ static __forceinline__ double get(const uint32_t (&pk)[DW], int k) { return (double)get_int(pk, k); }
+  __device__ static __forceinline__ int get_int(const uint32_t (&pk)[DW], int k) {
+    return (k < 3 ? field<0>(pk, k) : field<1>(pk, k - 3)) - 64;
+  }
 };
 // Trace basis (q2, 2, None): 25 digits in [-2, 2], 3 bits each (value + 2), 10 per dword.
 struct DigitsTrace {
@@ -134,19 +137,22 @@ __device__ __forceinline__ void cmux_step3(double (&acc0)[E], double (&acc1)[E],
       __builtin_amdgcn_wave_barrier();
       __atomic_signal_fence(__ATOMIC_SEQ_CST);
     }
+    // digit pairs (j, j + 3): the pair's two digits sit at the same offset of words 0 and 1.
+    // Products are counted in issue order g (reductions every fourth, as before; the sum is exact
+    // in any order), and the key row of the next digit in that order is loaded one digit ahead.
 #pragma unroll 1
-    for (int k2 = 0; k2 < D2; k2 += 2) {
+    for (int j = 0; j < D2 / 2; ++j) {
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        const int k = k2 + h, r = p * D2 + k;
-        double x[E];
-        int d[E];
+        const int g = p * D2 + 2 * j + h;  // issue order
+        int f[E];
 #pragma unroll
-        for (int e = 0; e < E; ++e) d[e] = DG::get_int(pk[e], k);
+        for (int e = 0; e < E; ++e) f[e] = h == 0 ? DG::template field<0>(pk[e], j) : DG::template field<1>(pk[e], j);
+        double x[E];
         if ((h ^ p) == 0)  // mask digits on X0, X1, ...; body digits on X1, X0, ...
-          NTT::template fwd_small<0>(d, t0, x, xch, tw, tid, gtw);
+          NTT::template fwd_small<0>(f, t0, x, xch, tw, tid, gtw);
         else
-          NTT::template fwd_small<1>(d, t0, x, xch, tw, tid, gtw);
+          NTT::template fwd_small<1>(f, t0, x, xch, tw, tid, gtw);
 #pragma unroll
         for (int e = 0; e < E; ++e) {
           accA[e] += mm<M>(x[e], (double)cur.a[e]);
@@ -154,14 +160,17 @@ __device__ __forceinline__ void cmux_step3(double (&acc0)[E], double (&acc1)[E],
         }
         // |x| <= 4.96q after the transform, so |mm(x, key)| <= 1.49q: four products on a
         // reduced sum stay below 6.5q < 2^53 (tests/test_fp64_residues.py)
-        if ((r % 4) == 3 && r + 1 < 2 * D2) {
+        if ((g % 4) == 3 && g + 1 < 2 * D2) {
 #pragma unroll
           for (int e = 0; e < E; ++e) {
             accA[e] = red<M>(accA[e]);
             accB[e] = red<M>(accB[e]);
           }
         }
-        if (r + 1 < 2 * D2) cur.load(ggsw + (size_t)(r + 1) * 2 * N, N, tid * E);
+        if (g + 1 < 2 * D2) {  // row of the next digit: (j, h = 1), (j + 1, h = 0) or the body's first
+          const int nr = h == 0 ? p * D2 + j + 3 : (j + 1 < D2 / 2 ? p * D2 + j + 1 : (p + 1) * D2);
+          cur.load(ggsw + (size_t)nr * 2 * N, N, tid * E);
+        }
       }
     }
   }

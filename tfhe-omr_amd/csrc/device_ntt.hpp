@@ -445,7 +445,8 @@ struct CmuxNtt {
     fwd_stages<0, 0, 3>(x, tw, tid, since_red);
     fwd_rest<XB>(x, lds, tw, tid, since_red);
   }
-  // Forward transform of a polynomial of small integer digits |d| <= 64: stages 0 and 1 from
+  // Forward transform of a polynomial of small integer digits |d| <= 64, given as fields
+  // f = d + 64 in [0, 128]: stages 0 and 1 from
   // five 129-entry LDS tables (t0 + 136 k: d * c_k for c = tw1, tw2, tw1 tw2, tw3, tw1 tw3)
   // instead of modular products. Stage 0 pairs (e, e + 4) under tw[1] for every thread; stage 1
   // pairs (e, e + 2) with tw[2] (e = 0, 1) and tw[3] (e = 4, 5), so tw2 * x[2] = tw2 d2 +
@@ -453,17 +454,17 @@ struct CmuxNtt {
   // (1.7q with the products), 6.84q before the stage-6 reduction: below 8q < 2^53 and inside mm's
   // exact range (replayed in tests/test_fp64_residues.py).
   template <int XB>
-  __device__ static __forceinline__ void fwd_small(const int (&d)[E], const double *t0, double (&x)[E],
+  __device__ static __forceinline__ void fwd_small(const int (&f)[E], const double *t0, double (&x)[E],
                                                    double *lds, const double *tw, int tid,
                                                    const double *__restrict__ gt) {
     const double *T1 = t0, *T2 = t0 + 136, *T3 = t0 + 272, *T4 = t0 + 408, *T5 = t0 + 544;
     // the ten table reads (an explicit sched_barrier forcing them all before the first use measured
     // 0.2 % slower)
-    double tv[10] = {T1[d[4] + 64], T1[d[5] + 64], T2[d[2] + 64], T3[d[6] + 64], T2[d[3] + 64],
-                     T3[d[7] + 64], T4[d[2] + 64], T5[d[6] + 64], T4[d[3] + 64], T5[d[7] + 64]};
+    double tv[10] = {T1[f[4]], T1[f[5]], T2[f[2]], T3[f[6]], T2[f[3]], T3[f[7]], T4[f[2]], T5[f[6]], T4[f[3]], T5[f[7]]};
     const double a4 = tv[0], a5 = tv[1];
-    const double x0 = (double)d[0] + a4, x4 = (double)d[0] - a4;
-    const double x1 = (double)d[1] + a5, x5 = (double)d[1] - a5;
+    const double d0 = (double)(f[0] - 64), d1 = (double)(f[1] - 64);
+    const double x0 = d0 + a4, x4 = d0 - a4;
+    const double x1 = d1 + a5, x5 = d1 - a5;
     const double v0 = tv[2] + tv[3], v1 = tv[4] + tv[5];
     const double v4 = tv[6] - tv[7], v5 = tv[8] - tv[9];
     x[0] = x0 + v0;

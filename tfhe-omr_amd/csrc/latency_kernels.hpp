@@ -220,31 +220,31 @@ __global__ __launch_bounds__(BR2L_T, 1) void br2l_kernel(const uint32_t *__restr
     KeyRow<double, E> cur;
     cur.load(ggsw, N, t * E);
 #pragma unroll 1
-    for (int k2 = 0; k2 < D2; k2 += 2) {
+    for (int j = 0; j < D2 / 2; ++j) {  // digit pairs (j, j + 3), as in cmux_step3
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        const int k = k2 + h;
+        const int s = 2 * j + h;  // issue order
         double x[E];
-        int d[E];
+        int f[E];
 #pragma unroll
-        for (int e = 0; e < E; ++e) d[e] = DG::get_int(pk[e], k);
+        for (int e = 0; e < E; ++e) f[e] = h == 0 ? DG::template field<0>(pk[e], j) : DG::template field<1>(pk[e], j);
         if (h == 0)  // digits on X0, X1, X0, ...
-          NTT::template fwd_small<0>(d, t0, x, X, tw, t, tb.tw2c);
+          NTT::template fwd_small<0>(f, t0, x, X, tw, t, tb.tw2c);
         else
-          NTT::template fwd_small<1>(d, t0, x, X, tw, t, tb.tw2c);
+          NTT::template fwd_small<1>(f, t0, x, X, tw, t, tb.tw2c);
 #pragma unroll
         for (int e = 0; e < E; ++e) {
           accA[e] += mm<M>(x[e], cur.a[e]);
           accB[e] += mm<M>(x[e], cur.b[e]);
         }
-        if (k == 3) {  // four products on a reduced sum stay below 6.5q (cmux_step3)
+        if (s == 3) {  // four products on a reduced sum stay below 6.5q (cmux_step3)
 #pragma unroll
           for (int e = 0; e < E; ++e) {
             accA[e] = red<M>(accA[e]);
             accB[e] = red<M>(accB[e]);
           }
         }
-        if (k + 1 < D2) cur.load(ggsw + (size_t)(k + 1) * 2 * N, N, t * E);
+        if (s + 1 < D2) cur.load(ggsw + (size_t)(h == 0 ? j + 3 : j + 1) * 2 * N, N, t * E);
       }
     }
     // exchange the partial the other group owns: group 0 sends B, group 1 sends A
