@@ -62,17 +62,17 @@ def test_level1_unsigned_min_canon():
     assert np.array_equal(got, _centred(x, q))
 
 
-def test_level2_forward_ntt_bound_with_stage01_tables():
-    """device_ntt.hpp fwd3_small (OMR_NTT_T0 = 2): after stages 0 and 1 from the tables (each
-    entry canonical) |x| <= |d| + 3 (q - 1) / 2 <= 2q; stages 2..5 each add mm(x, w) with
-    |mm| <= (0.5 + A/5) q for |x| <= A q, and the reduction comes before stage 6. The largest
-    value must stay below 2^53 = 8q (q2 < 2^50); the mm bound itself is replayed in FP64."""
+def _mm_bound(a):
+    """|mm(a, w)| / q for |a| <= A q, |w| <= (q - 1) / 2 (device_ntt.hpp mm): the quotient
+    rint(fl(h * fl(1/q))) errs by at most 0.5 + 2^-52 |h / q| (three roundings), and the low part l
+    of the error-free product adds |h| 2^-53: with q < 2^50 that is (0.5 + 0.125 A + 0.0625 A)."""
+    return 0.5 + 0.1875 * a
+
+
+def _replay_mm(bound, seed):
+    """mm on operands up to bound * q: exact residue, no intermediate above 2^53, within _mm_bound."""
     q = Q2
-    bound = 2.0
-    for _ in range(4):  # stages 2, 3, 4, 5
-        bound += 0.5 + bound / 5
-    assert bound * q < 2.0**53 and bound < 6.9
-    rng = np.random.default_rng(14)
+    rng = np.random.default_rng(seed)
     n = 20_000
     a = np.rint(rng.uniform(-bound, bound, n) * q)
     a[:2] = (-np.floor(bound * q), np.floor(bound * q))
@@ -86,21 +86,51 @@ def test_level2_forward_ntt_bound_with_stage01_tables():
         r = (hh - e * q) + (x * y - hh)
         assert abs(hh - e * q) < 2**53 and abs(r) < 2**53
         assert r % q == (x * y) % q
-        assert abs(r) <= (0.5 + bound / 5) * q
+        assert abs(r) <= _mm_bound(bound) * q
+
+
+def _stage(a_u, a_v):
+    """CT butterfly u +- mm(v, w): the output bound from the operand bounds."""
+    return a_u + _mm_bound(a_v)
+
+
+def test_level2_forward_ntt_bound_with_stage01_tables():
+    """device_ntt.hpp CmuxNtt::fwd_small: after stages 0 and 1 from the tables (each entry
+    canonical) |x| <= |d| + 3 (q - 1) / 2 <= 1.5q + 64; stages 2..5 each add mm(x, w); before
+    stage 6 only the u operands are reduced (|u| <= q/2 + 2), the v operands go into mm as they
+    are; stages 6..10 follow. Every value stays below 2^53 = 8q (q2 < 2^50); the mm bound is
+    replayed in FP64 at the largest operands (5.62q before stage 6, 6.72q at the output)."""
+    q = Q2
+    b = 1.5 + 64 / q
+    for _ in range(4):  # stages 2, 3, 4, 5
+        b = _stage(b, b)
+    assert 5.6 < b < 5.63
+    red = 0.5 + 2 / q
+    b = _stage(red, b)  # stage 6: reduced u, unreduced v
+    for _ in range(4):  # stages 7..10
+        b = _stage(b, b)
+    assert 6.7 < b < 6.73 and b * q < 2.0**53
+    _replay_mm(5.63, 14)
+    _replay_mm(6.73, 15)
+    # the key conversion (CmuxNtt::fwd from canonical residues) has the same shape
+    k = 0.5
+    for _ in range(6):
+        k = _stage(k, k)
+    k = _stage(red, k)
+    for _ in range(4):
+        k = _stage(k, k)
+    assert k < 7.0
 
 
 def test_level2_mac_four_products_per_reduction():
-    """detect_kernels.hpp cmux_step3 (OMR_MAC_RED4): the forward transform ends 5 stages after
-    its reduction (|x| <= q/2 + 2 there), so |x| <= 4.96q; with |key| <= q/2 each product
-    |mm(x, key)| <= (0.5 + 4.96/5) q, and a reduced sum (|acc| <= q/2 + 2) plus four products
-    stays below 8q < 2^53. A fifth product would not fit."""
-    b = 0.5
-    for _ in range(5):  # stages 6..10
-        b += 0.5 + b / 5
-    assert 4.9 < b < 4.97
-    prod = 0.5 + b / 5
-    assert 0.5 + 4 * prod < 6.5 and (0.5 + 4 * prod) * Q2 < 2.0**53
-    assert (0.5 + 5 * prod) * Q2 > 2.0**53 * 0.99  # no margin for five
+    """detect_kernels.hpp cmux_step3: the forward transform output is |x| <= 6.72q, so each
+    product |mm(x, key)| <= 1.76q (|key| <= q/2), and a reduced sum (|acc| <= q/2 + 2) plus four
+    products stays below 7.6q < 8q < 2^53. A fifth product would not fit."""
+    b = 6.73
+    prod = _mm_bound(b)
+    assert prod < 1.77
+    assert (0.5 + 4 * prod) < 7.6 and (0.5 + 4 * prod) * Q2 < 2.0**53
+    assert (0.5 + 5 * prod) * Q2 > 2.0**53
 
 
 def test_inverse_twiddles_mirror_forward_table():

@@ -158,8 +158,8 @@ __device__ __forceinline__ void cmux_step3(double (&acc0)[E], double (&acc1)[E],
           accA[e] += mm<M>(x[e], (double)cur.a[e]);
           accB[e] += mm<M>(x[e], (double)cur.b[e]);
         }
-        // |x| <= 4.96q after the transform, so |mm(x, key)| <= 1.49q: four products on a
-        // reduced sum stay below 6.5q < 2^53 (tests/test_fp64_residues.py)
+        // |x| <= 6.72q after the transform, so |mm(x, key)| <= 1.76q: four products on a
+        // reduced sum stay below 7.6q < 8q < 2^53 (tests/test_fp64_residues.py)
         if ((g % 4) == 3 && g + 1 < 2 * D2) {
 #pragma unroll
           for (int e = 0; e < E; ++e) {

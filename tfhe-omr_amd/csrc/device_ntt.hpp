@@ -352,8 +352,12 @@ struct CmuxNtt {
                                                const double *__restrict__ gt = nullptr) {
     constexpr int h = 1 << rbit(P, L - 1 - S);
     if (since_red >= (INV ? M::RED_INV : M::RED_FWD)) {
+      // forward: only the u operands (x[e], e & h == 0) are reduced; mm takes the v operands as
+      // they are (|v| <= 6.3q, |mm| <= 1.7q), which keeps the transform output below 7q
+      // (bounds in tests/test_fp64_residues.py)
 #pragma unroll
-      for (int e = 0; e < E; ++e) x[e] = red<M>(x[e]);
+      for (int e = 0; e < E; ++e)
+        if (INV || !(e & h)) x[e] = red<M>(x[e]);
       since_red = 0;
     }
 #pragma unroll
@@ -450,9 +454,9 @@ struct CmuxNtt {
   // five 129-entry LDS tables (t0 + 136 k: d * c_k for c = tw1, tw2, tw1 tw2, tw3, tw1 tw3)
   // instead of modular products. Stage 0 pairs (e, e + 4) under tw[1] for every thread; stage 1
   // pairs (e, e + 2) with tw[2] (e = 0, 1) and tw[3] (e = 4, 5), so tw2 * x[2] = tw2 d2 +
-  // tw1 tw2 d6 and tw3 * x[6] = tw3 d2 - tw1 tw3 d6 are table sums. Bound: |x| <= 2q after stage 1
-  // (1.7q with the products), 6.84q before the stage-6 reduction: below 8q < 2^53 and inside mm's
-  // exact range (replayed in tests/test_fp64_residues.py).
+  // tw1 tw2 d6 and tw3 * x[6] = tw3 d2 - tw1 tw3 d6 are table sums. Bound: |x| <= 1.5q + 64 after
+  // stage 1, 5.62q before the stage-6 (u-operand) reduction, 6.72q at the output: below 8q < 2^53
+  // and inside mm's exact range (replayed in tests/test_fp64_residues.py).
   template <int XB>
   __device__ static __forceinline__ void fwd_small(const int (&f)[E], const double *t0, double (&x)[E],
                                                    double *lds, const double *tw, int tid,

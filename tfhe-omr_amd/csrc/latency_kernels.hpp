@@ -237,7 +237,7 @@ __global__ __launch_bounds__(BR2L_T, 1) void br2l_kernel(const uint32_t *__restr
           accA[e] += mm<M>(x[e], cur.a[e]);
           accB[e] += mm<M>(x[e], cur.b[e]);
         }
-        if (s == 3) {  // four products on a reduced sum stay below 6.5q (cmux_step3)
+        if (s == 3) {  // four products on a reduced sum stay below 7.6q (cmux_step3)
 #pragma unroll
           for (int e = 0; e < E; ++e) {
             accA[e] = red<M>(accA[e]);
