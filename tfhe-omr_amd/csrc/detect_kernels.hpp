@@ -78,6 +78,17 @@ __device__ __forceinline__ double rot_read(const double *p, int j, int r) {
   return s * p[t];
 }
 
+// (X^r * p)[j] for p in LDS as t = (j - r) mod 2N: p[t] for t < N, -p[t - N] above (the sign
+// flipped by one xor of bit 63 instead of compare/select pairs and a multiply).
+template <int N>
+__device__ __forceinline__ double rot_read_lds(const double *p, int j, int r) {
+  static_assert((N & (N - 1)) == 0 && N <= (1 << 20), "power-of-two ring degree");
+  const uint32_t t = (uint32_t)(j - r) & (2 * N - 1);
+  const double v = p[t & (N - 1)];
+  const uint32_t hi = (uint32_t)(__builtin_bit_cast(uint64_t, v) >> 32) ^ ((t & N) << (31 - ilog2(N)));
+  return __builtin_bit_cast(double, (__builtin_bit_cast(uint64_t, v) & 0xffffffffull) | ((uint64_t)hi << 32));
+}
+
 }  // namespace omr
 
 #include "br1_fft.hpp"
@@ -133,7 +144,7 @@ __device__ __forceinline__ void cmux_step3(double (&acc0)[E], double (&acc1)[E],
       __syncthreads();
 #pragma unroll
       for (int e = 0; e < E; ++e)
-        DG::pack(canon_small<M>(rot_read<N>(st, tid + e * T, a) - (p == 0 ? acc0[e] : acc1[e])), pk[e]);
+        DG::pack(canon_small<M>(rot_read_lds<N>(st, tid + e * T, a) - (p == 0 ? acc0[e] : acc1[e])), pk[e]);
       __builtin_amdgcn_wave_barrier();
       __atomic_signal_fence(__ATOMIC_SEQ_CST);
     }

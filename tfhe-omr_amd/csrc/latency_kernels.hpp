@@ -210,7 +210,7 @@ __global__ __launch_bounds__(BR2L_T, 1) void br2l_kernel(const uint32_t *__restr
       for (int e = 0; e < E; ++e) st[t + e * T] = acc[e];
       __syncthreads();
 #pragma unroll
-      for (int e = 0; e < E; ++e) DG::pack(canon_small<M>(rot_read<N>(st, t + e * T, a) - acc[e]), pk[e]);
+      for (int e = 0; e < E; ++e) DG::pack(canon_small<M>(rot_read_lds<N>(st, t + e * T, a) - acc[e]), pk[e]);
       __builtin_amdgcn_wave_barrier();
       __atomic_signal_fence(__ATOMIC_SEQ_CST);
     }
