@@ -42,11 +42,16 @@ struct Lvl1Int {
   __device__ static __forceinline__ uint32_t digits(int v) {
     return (uint32_t)(((v + (1 << (DROP1 - 1))) >> DROP1) + DIGIT_BIAS) ^ (uint32_t)DIGIT_BIAS;
   }
-  // signed digit k of a digits() word: two wave-uniform shifts (field to the top, arithmetic
-  // shift down). A v_bfe_i32 in inline asm is slower (it constrains the scheduler), and
-  // __builtin_amdgcn_sbfe with a run-time width is miscompiled by ROCm 7.2 (v_cvt_f64_u32).
+  // signed digit k of a digits() word: one v_bfe_i32 with wave-uniform offset and width
+  // (checked in the listing: v_bfe_i32 + v_cvt_f64_i32; an inline-asm v_bfe_i32 is slower, it
+  // constrains the scheduler).
   __device__ static __forceinline__ double digit(uint32_t w, int k) {
     return (double)(int)__builtin_amdgcn_sbfe(w, LOGB1 * k, k < D1 - 1 ? LOGB1 : 32 - LOGB1 * (D1 - 1));
+  }
+  // the same digit by two shifts (the latency kernel measured 1-2 % faster with these)
+  __device__ static __forceinline__ double digit_shifts(uint32_t w, int k) {
+    const int s1 = k < D1 - 1 ? 32 - LOGB1 * (k + 1) : 0, s2 = k < D1 - 1 ? 32 - LOGB1 : LOGB1 * (D1 - 1);
+    return (double)((int)(w << s1) >> s2);
   }
 };
 

@@ -92,7 +92,7 @@ __global__ __launch_bounds__(64 * BR1L_WAVES, 1) void br1l_kernel(
         const int j = acc_coef(lane, q);
         const uint32_t w = Lvl1Int::digits(
             Lvl1Int::canon(ext[p][(base + acc_coef(0, q)) & (2 * N1 - 1)] - ext[p][j]));
-        const double d = Lvl1Int::digit(w, wave);
+        const double d = Lvl1Int::digit_shifts(w, wave);
         if (q < 8)
           xr[p][q] = d;
         else
@@ -219,15 +219,17 @@ __global__ __launch_bounds__(BR2L_T, 1) void br2l_kernel(const uint32_t *__restr
     for (int e = 0; e < E; ++e) accA[e] = accB[e] = 0.0;
     KeyRow<double, E> cur;
     cur.load(ggsw, N, t * E);
+    // digits in order (the throughput kernel's (j, j + 3) pairing measured 6 % slower here: its
+    // row choice splits the loop body into blocks the scheduler cannot overlap)
 #pragma unroll 1
-    for (int j = 0; j < D2 / 2; ++j) {  // digit pairs (j, j + 3), as in cmux_step3
+    for (int k2 = 0; k2 < D2; k2 += 2) {
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        const int s = 2 * j + h;  // issue order
+        const int k = k2 + h;
         double x[E];
         int f[E];
 #pragma unroll
-        for (int e = 0; e < E; ++e) f[e] = h == 0 ? DG::template field<0>(pk[e], j) : DG::template field<1>(pk[e], j);
+        for (int e = 0; e < E; ++e) f[e] = DG::get_int(pk[e], k) + 64;
         if (h == 0)  // digits on X0, X1, X0, ...
           NTT::template fwd_small<0>(f, t0, x, X, tw, t, tb.tw2c);
         else
@@ -237,14 +239,14 @@ __global__ __launch_bounds__(BR2L_T, 1) void br2l_kernel(const uint32_t *__restr
           accA[e] += mm<M>(x[e], cur.a[e]);
           accB[e] += mm<M>(x[e], cur.b[e]);
         }
-        if (s == 3) {  // four products on a reduced sum stay below 7.6q (cmux_step3)
+        if (k == 3) {  // four products on a reduced sum stay below 7.6q (cmux_step3)
 #pragma unroll
           for (int e = 0; e < E; ++e) {
             accA[e] = red<M>(accA[e]);
             accB[e] = red<M>(accB[e]);
           }
         }
-        if (s + 1 < D2) cur.load(ggsw + (size_t)(h == 0 ? j + 3 : j + 1) * 2 * N, N, t * E);
+        if (k + 1 < D2) cur.load(ggsw + (size_t)(k + 1) * 2 * N, N, t * E);
       }
     }
     // exchange the partial the other group owns: group 0 sends B, group 1 sends A
