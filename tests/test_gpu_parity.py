@@ -142,6 +142,30 @@ def test_real_keys_stage_parity(real, path):
     assert np.array_equal(det.second_level(fl[:1])[0], orc.trace(br[0]))
 
 
+def test_latency_level2_variants_match_throughput(real):
+    """The latency path's level 2 in both forms against the (oracle-checked) throughput kernels,
+    bit for bit: the two-CU kernel br2x at 64 messages (128 workgroups, the default threshold's
+    largest chunk) and the one-CU kernel br2l, which runs when 2 n workgroups exceed the CU count
+    (130 messages with the threshold raised); every output passes the omd KAT."""
+    a, det, _ = real
+    s2 = a.export()["s2"]
+    for n, threshold in ((64, 64), (130, 200)):
+        mask = np.zeros(n, dtype=bool)
+        mask[::9] = True
+        ca, cb = PL.mixed_clues(mask, seed=900 + n)
+        det.set_latency_threshold(threshold)
+        try:
+            lat = det.detect_batch(ca, cb)
+        finally:
+            det.set_latency_threshold(0)
+        thr = det.detect_batch(ca, cb)
+        det.set_latency_threshold(64)
+        assert np.array_equal(lat, thr)
+        for m in range(n):
+            dec = R.decrypt_decode(s2, lat[m])
+            assert (dec[0] == 1) == mask[m] and not dec[1:].any()
+
+
 def test_encode_golden(structured):
     det, _ = structured
     z = np.load(os.path.join(GOLDEN, "encode.npz"))

@@ -138,6 +138,13 @@ struct omr_ctx {
   // chunks of at most latency_max messages run the latency kernels (latency_kernels.hpp)
   size_t latency_max = OMR_DEFAULT_LATENCY_MAX;
   int *ks_part = nullptr;  // split key-switch partial sums, [KS_SPLIT][64][672][4]
+  // two-CU level-2 latency kernel (br2x_kernel): partial hand-off slots [n][2][2][N2], flags
+  // [n][2], a sticky timeout flag; used when 2 n workgroups fit the CUs at once
+  double *x_slots = nullptr;
+  uint32_t *x_flags = nullptr;
+  int *x_err = nullptr;
+  size_t x_cap = 0;
+  int num_cu = 0;
   // host-API staging
   uint16_t *s_clue_a = nullptr, *s_clue_b = nullptr;
   uint64_t *s_out = nullptr;
@@ -294,6 +301,17 @@ omr_status convert_keys_fft1(const uint32_t *host, size_t npoly, double2 *dev, c
 
 bool latency_path(const omr_ctx *c, size_t n) { return n <= c->latency_max; }
 
+// br2x_kernel's bounded hand-off wait: a workgroup whose partner never published leaves its loop
+// and sets x_err (sticky; reported by the next host-API detect after its stream sync).
+omr_status check_handoff(omr_ctx *c) {
+  if (!c->x_err) return OMR_OK;
+  int e = 0;
+  HIP_TRY(hipMemcpy(&e, c->x_err, sizeof(int), hipMemcpyDeviceToHost));
+  if (!e) return OMR_OK;
+  HIP_TRY(hipMemset(c->x_err, 0, sizeof(int)));
+  return set_error(OMR_ERR_DEVICE, "level-2 two-CU hand-off timed out (workgroups not co-resident)");
+}
+
 // LWE key switch + modulus switch of B messages (lwe1t [1025][B] -> out [B][671]). Up to 64
 // messages (the latency path) the input coefficients are split over KS_SPLIT workgroup slices.
 omr_status launch_ks(omr_ctx *c, int B, uint32_t *out, hipStream_t st) {
@@ -326,8 +344,28 @@ omr_status launch_br1(omr_ctx *c, size_t n, const uint16_t *ca, const uint16_t *
 // Level-2 blind rotation (+ trace, mode 0) of n LWE(670, 4096) ciphertexts, one workgroup each.
 omr_status launch_br2(omr_ctx *c, size_t n, const uint32_t *lwe_int, uint64_t *out, int mode,
                       hipStream_t st) {
-  if (latency_path(c, n)) {  // two 4-wave groups per message, then the trace in place
-    br2l_kernel<<<(unsigned)n, BR2L_T, 0, st>>>(lwe_int, c->bsk2, c->tb, out);
+  if (latency_path(c, n)) {  // two CUs (or two 4-wave groups) per message, then the trace in place
+    if (2 * n <= (size_t)c->num_cu) {  // every workgroup resident at once (one per CU)
+      if (n > c->x_cap) {
+        omr_status s;
+        if ((s = scratch_idle(c)) != OMR_OK) return s;
+        dev_free(c->x_slots);
+        dev_free(c->x_flags);
+        c->x_cap = 0;
+        HIP_TRY(hipMalloc(&c->x_slots, n * 4 * N2 * sizeof(double)));
+        HIP_TRY(hipMalloc(&c->x_flags, n * 2 * sizeof(uint32_t)));
+        if (!c->x_err) {
+          HIP_TRY(hipMalloc(&c->x_err, sizeof(int)));
+          HIP_TRY(hipMemsetAsync(c->x_err, 0, sizeof(int), st));
+        }
+        c->x_cap = n;
+      }
+      HIP_TRY(hipMemsetAsync(c->x_flags, 0, n * 2 * sizeof(uint32_t), st));
+      br2x_kernel<<<(unsigned)(2 * n), BR2L_T, 0, st>>>(lwe_int, c->bsk2, c->tb, c->x_slots, c->x_flags,
+                                                        c->x_err, out);
+    } else {
+      br2l_kernel<<<(unsigned)n, BR2L_T, 0, st>>>(lwe_int, c->bsk2, c->tb, out);
+    }
     if (mode == 0) {
       HIP_TRY(hipGetLastError());
       trace_kernel<<<(unsigned)n, BR2_T, 0, st>>>(out, c->tk, c->tb);
@@ -360,6 +398,7 @@ extern "C" omr_status omr_ctx_create(const omr_detection_key_view *key, int devi
   HIP_TRY(hipSetDevice(device));
   auto *c = new omr_ctx();
   c->device = device;
+  HIP_TRY(hipDeviceGetAttribute(&c->num_cu, hipDeviceAttributeMultiprocessorCount, device));
   auto fail = [&](omr_status st) {
     omr_ctx_destroy(c);
     return st;
@@ -470,6 +509,9 @@ extern "C" void omr_ctx_destroy(omr_ctx *c) {
   dev_free(c->s_out);
   dev_free(c->partial);
   dev_free(c->ks_part);
+  dev_free(c->x_slots);
+  dev_free(c->x_flags);
+  dev_free(c->x_err);
   for (auto e : c->events) (void)hipEventDestroy(e);
   if (c->scratch_free) (void)hipEventDestroy(c->scratch_free);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -590,6 +632,7 @@ extern "C" omr_status omr_detect_batch(omr_ctx *c, const uint16_t *ca, const uin
     if ((s = detect_device(c, c->s_clue_a, c->s_clue_b, n, c->s_out, c->stream)) != OMR_OK) return s;
     HIP_TRY(hipMemcpyAsync(out + off * 2 * N2, c->s_out, n * 2 * N2 * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
+    if ((s = check_handoff(c)) != OMR_OK) return s;
     if (c->timing) {
       omr_detect_timing t;
       if ((s = collect_timing(c, &t)) != OMR_OK) return s;

@@ -265,6 +265,165 @@ __global__ __launch_bounds__(BR2L_T, 1) void br2l_kernel(const uint32_t *__restr
   for (int e = 0; e < E; ++e) o[t + e * T] = to_u64<M>(acc[e]);
 }
 
+// ---- level 2 over two CUs per message --------------------------------------------------------
+// Workgroup 2m + r owns polynomial r (0 mask, 1 body) of message m and its accumulator: its two
+// 256-thread groups transform digits 3g .. 3g + 2 of that polynomial (GGSW rows r D2 + 3g + ..)
+// and multiply-accumulate both outputs; group 1's partials join group 0's through LDS; the
+// output the partner owns (mask CU: B, body CU: A) crosses to it through global memory and the
+// partner's arrives the same way; group 0 runs the inverse transform and updates ACC_r. Half the
+// transforms of br2l_kernel per CU and step, plus one hand-off.
+// Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility, the first row of the sc1 table):
+// every storing thread stores its payload with sc1 stores (agent-scope relaxed atomics) and waits
+// vmcnt(0); a workgroup barrier; one lane stores the sc1 flag (step + 1). The consumer's lane 0
+// polls the partner's flag with sc1 loads, a workgroup barrier follows, and every load of the
+// payload is an sc1 load. Payload slots alternate by step parity (the partner cannot publish two
+// steps ahead: each step needs the other's previous partial). The poll is bounded: after
+// BR2X_SPIN polls the workgroup records an error in *err and leaves the loop, so every wave
+// exits. The grid (2 workgroups per message, one per CU) must be co-resident: the launch checks
+// it against the CU count.
+constexpr int BR2X_SPIN = 1 << 24;
+
+__device__ __forceinline__ void st_sc1(double *p, double v) {
+  __hip_atomic_store(reinterpret_cast<uint64_t *>(p), __builtin_bit_cast(uint64_t, v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_sc1(const double *p) {
+  return __builtin_bit_cast(double, __hip_atomic_load(reinterpret_cast<const uint64_t *>(p), __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT));
+}
+
+__global__ __launch_bounds__(BR2L_T, 1) void br2x_kernel(const uint32_t *__restrict__ lwe_int,
+                                                         const double *__restrict__ bsk2, DeviceTables tb,
+                                                         double *xg, uint32_t *flags, int *err,
+                                                         uint64_t *__restrict__ out) {
+  using M = Mod<2>;
+  constexpr int T = BR2_T, E = BR2_E, N = N2;
+  using NTT = CmuxNtt;
+  using DG = Digits2;
+  constexpr int KD = D2 / 2;  // digits per group
+  __shared__ double xbuf[2][NTT::LDS_DOUBLES];
+  __shared__ double part[2][N];
+  __shared__ double tws[N + 136 * 5];
+  __shared__ int stop;
+  const int m = blockIdx.x >> 1, r = blockIdx.x & 1;
+  const int g = threadIdx.x / T, t = threadIdx.x % T;
+  double *X = xbuf[g];
+  double *ST = xbuf[0] + N;  // the staged accumulator (group 0's X1), read by both groups
+  const double *tw = tws, *t0 = tws + N;
+  const uint32_t *lwe = lwe_int + (size_t)m * (NI + 1);
+  double acc[E];  // ACC_r, group 0 only
+  {
+    const int b = (int)lwe[NI];
+    const int rr = (2 * N - (b % (2 * N))) % (2 * N);
+#pragma unroll
+    for (int e = 0; e < E; ++e) acc[e] = r == 1 ? canon_small<M>(rot_read<N>(tb.lut2, t + e * T, rr)) : 0.0;
+    for (int j = threadIdx.x; j < N; j += BR2L_T) tws[j] = tb.tw2c[j];
+    if (threadIdx.x <= 128) {  // table k: d * c_k, d = tid - 64 (c = tw1, tw2, tw1 tw2, tw3, tw1 tw3)
+      const double w1 = tb.tw2[1], w2 = tb.tw2[2], w3 = tb.tw2[3];
+      const double c[5] = {w1, w2, canon<M>(mm<M>(w1, w2)), w3, canon<M>(mm<M>(w1, w3))};
+#pragma unroll
+      for (int k = 0; k < 5; ++k)
+        tws[N + 136 * k + threadIdx.x] = canon<M>(mm<M>((double)((int)threadIdx.x - 64), c[k]));
+    }
+    if (threadIdx.x == 0) stop = 0;
+    __syncthreads();
+  }
+  uint32_t *my_flag = flags + 2 * m + r, *their_flag = flags + 2 * m + (1 - r);
+#pragma unroll 1
+  for (int i = 0; i < NI; ++i) {
+    const int a = (int)__builtin_amdgcn_readfirstlane(lwe[i]) & (2 * N - 1);
+    if (a == 0) continue;  // (X^0 - 1) * ACC = 0 (both workgroups of the message skip it)
+    const double *ggsw = bsk2 + ((size_t)i * 2 * D2 + (size_t)r * D2 + (size_t)g * KD) * 2 * N;
+    uint32_t pk[E][DG::DW];
+    {  // digits of (X^a - 1) * ACC_r: group 0 stages ACC_r, both groups decompose it
+      if (g == 0) {
+#pragma unroll
+        for (int e = 0; e < E; ++e) ST[t + e * T] = acc[e];
+      }
+      __syncthreads();
+#pragma unroll
+      for (int e = 0; e < E; ++e)
+        DG::pack(canon_small<M>(rot_read_lds<N>(ST, t + e * T, a) - ST[t + e * T]), pk[e]);
+      __builtin_amdgcn_wave_barrier();
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    }
+    double accA[E], accB[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) accA[e] = accB[e] = 0.0;
+    KeyRow<double, E> cur;
+    cur.load(ggsw, N, t * E);
+#pragma unroll
+    for (int h = 0; h < KD; ++h) {  // three digits: X0, X1, X0 (the staging used group 0's X1)
+      const int k = g * KD + h;
+      double x[E];
+      int f[E];
+#pragma unroll
+      for (int e = 0; e < E; ++e) f[e] = DG::get_int(pk[e], k) + 64;
+      if ((h & 1) == 0)
+        NTT::template fwd_small<0>(f, t0, x, X, tw, t, tb.tw2c);
+      else
+        NTT::template fwd_small<1>(f, t0, x, X, tw, t, tb.tw2c);
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        accA[e] += mm<M>(x[e], cur.a[e]);
+        accB[e] += mm<M>(x[e], cur.b[e]);
+      }
+      if (h + 1 < KD) cur.load(ggsw + (size_t)(h + 1) * 2 * N, N, t * E);
+    }
+    // group 1's partials join group 0's (three products on a zero sum: |.| < 5.3q)
+    if (g == 1) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        part[0][t * E + e] = red<M>(accA[e]);
+        part[1][t * E + e] = red<M>(accB[e]);
+      }
+    }
+    __syncthreads();
+    double keep[E];
+    if (g == 0) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const double sa = red<M>(red<M>(accA[e]) + part[0][t * E + e]);
+        const double sb = red<M>(red<M>(accB[e]) + part[1][t * E + e]);
+        keep[e] = r == 0 ? sa : sb;
+        st_sc1(xg + (((size_t)m * 2 + r) * 2 + (i & 1)) * N + t * E + e, r == 0 ? sb : sa);  // the partner's output
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __hip_atomic_store(my_flag, (uint32_t)(i + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      int n = 0;
+      while (__hip_atomic_load(their_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (uint32_t)(i + 1)) {
+        if (++n == BR2X_SPIN) {
+          stop = 1;
+          atomicExch(err, 1);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+    }
+    __syncthreads();
+    if (stop) break;
+    if (g == 0) {
+      double s[E];
+#pragma unroll
+      for (int e = 0; e < E; ++e)
+        s[e] = red<M>(keep[e] + ld_sc1(xg + (((size_t)m * 2 + (1 - r)) * 2 + (i & 1)) * N + t * E + e));
+      NTT::template inv<0>(s, X, tw, t, tb.tw2c);
+#pragma unroll
+      for (int e = 0; e < E; ++e) acc[e] = canon<M>(acc[e] + s[e]);
+    } else {
+      __syncthreads();  // the inverse's one workgroup barrier (its cross-wave exchange)
+    }
+  }
+  if (g == 0) {
+    uint64_t *o = out + (size_t)m * 2 * N + (size_t)r * N;
+#pragma unroll
+    for (int e = 0; e < E; ++e) o[t + e * T] = to_u64<M>(acc[e]);
+  }
+}
+
 // hom_trace (detector.rs:626-639) in place on blind-rotation outputs (coefficient domain,
 // canonical u64 [2][N2] per message) -> NttRlweCiphertext u64 [2][N2].
 __global__ __launch_bounds__(BR2_T, 2) void trace_kernel(uint64_t *__restrict__ io, const double *__restrict__ tk,
