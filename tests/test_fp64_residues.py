@@ -149,3 +149,24 @@ def test_inverse_twiddles_mirror_forward_table():
         for j in range(1 << s):
             itw = pow(psi, (4096 - brv((1 << s) + j)) % 4096, q)
             assert itw == (q - tw[(2 << s) - 1 - j]) % q
+
+
+def test_level1_magic_round_reduce():
+    """br1_fft.hpp Lvl1Int::round_red: for y = integer + e (|y| < 2^43, |e| < 0.01, an FFT product
+    output), r = y - rint(y / q) q keeps the fraction exactly, and the low 32 bits of r + 1.5 * 2^52
+    are round(r) = round(y) mod q (centred, |.| <= (q + 1) / 2) in two's complement."""
+    q = Q1
+    rng = np.random.default_rng(15)
+    n = 400_000
+    ints = np.concatenate([rng.integers(-(1 << 43) + 1, 1 << 43, n), np.arange(-3000, 3000),
+                           rng.integers(-(1 << 43) // q, (1 << 43) // q, 20_000) * q + (q - 1) // 2])
+    e = rng.uniform(-0.01, 0.01, ints.size)
+    y = ints.astype(np.float64) + e
+    k = np.rint(y * (1.0 / q))
+    r = y - k * q  # exact here, as the device's fma
+    t = r + 6755399441055744.0
+    low = (t.view(np.uint64) & 0xFFFFFFFF).astype(np.int64)
+    got = np.where(low >= 1 << 31, low - (1 << 32), low)
+    want = _centred(ints, q)
+    assert np.all(np.abs(got) <= (q + 1) // 2)
+    assert np.array_equal(np.mod(got, q), np.mod(want, q))

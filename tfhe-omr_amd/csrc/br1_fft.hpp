@@ -31,6 +31,14 @@ struct Lvl1Int {
     return (int)y - H;
   }
   __device__ static __forceinline__ uint32_t to_u32(int x) { return (uint32_t)(x < 0 ? x + Q : x); }
+  // y = an integer + e (|y| < 2^43, |e| < 0.01: an FFT product output): round(y) mod q, centred,
+  // as an int. The quotient is rint(y / q) and r = y - kq keeps the fraction; adding 1.5 * 2^52
+  // rounds r to the nearest integer in the low mantissa bits, which are its two's complement
+  // (|round(r)| <= H + 1): one FP64 add instead of rint + conversion.
+  __device__ static __forceinline__ int round_red(double y) {
+    const double r = __fma_rn(-rint(y * (1.0 / 134215681.0)), 134215681.0, y);
+    return (int)(uint32_t)__builtin_bit_cast(uint64_t, r + 6755399441055744.0);
+  }
   // NonPowOf2ApproxSignedBasis (logB 5, d 4, drop 7) on a canonical residue: y = floor((v + 2^6)
   // / 2^7) has balanced base-32 digits d_k in [-16, 15] (k < 3) and an unbounded top digit; in
   // closed form, with y' = y + 16 (1 + 32 + 32^2): d_k = ((y' >> 5k) & 31) - 16 for k < 3 and
@@ -189,8 +197,7 @@ __device__ __forceinline__ void br1f_step_lds(uint32_t (&ac)[2][16], double2 *xc
     F::inv<1, true>(outr[o], outi[o], xch, tws, lane, gtw);
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      const double v = rint(i < 8 ? outr[o][0][i] : outi[o][0][i - 8]);  // exact (< 2^43)
-      ac[o][i] = Lvl1Off::add(ac[o][i], (int)red<Mod<1>>(v));
+      ac[o][i] = Lvl1Off::add(ac[o][i], Lvl1Int::round_red(i < 8 ? outr[o][0][i] : outi[o][0][i - 8]));
     }
   }
 }
