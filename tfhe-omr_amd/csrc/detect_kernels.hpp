@@ -190,12 +190,12 @@ __device__ __forceinline__ void cmux_step3(double (&acc0)[E], double (&acc1)[E],
     accA[e] = red<M>(accA[e]);
     accB[e] = red<M>(accB[e]);
   }
-  NTT::template inv<1>(accA, xch, tw, tid, gtw);
+  NTT::inv2(accA, accB, xch, tw, tid, gtw);  // A through X1, then B through X0
 #pragma unroll
-  for (int e = 0; e < E; ++e) acc0[e] = canon<M>(acc0[e] + accA[e]);
-  NTT::template inv<0>(accB, xch, tw, tid, gtw);
-#pragma unroll
-  for (int e = 0; e < E; ++e) acc1[e] = canon<M>(acc1[e] + accB[e]);
+  for (int e = 0; e < E; ++e) {
+    acc0[e] = canon<M>(acc0[e] + accA[e]);
+    acc1[e] = canon<M>(acc1[e] + accB[e]);
+  }
 }
 
 // Sum of the 7 extracted LWEs mod q1 (detector.rs:556), transposed to [N1+1][B] for the key

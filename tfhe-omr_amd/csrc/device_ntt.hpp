@@ -483,6 +483,28 @@ struct CmuxNtt {
     fwd_stages<0, 2, 3, true>(x, tw, tid, since_red, gt);
     fwd_rest<XB>(x, lds, tw, tid, since_red);
   }
+  // Two unscaled inverses interleaved (the CMUX step's outputs A and B) for instruction-level
+  // parallelism: the wave-local exchanges run one after the other through W; the cross-wave
+  // exchanges keep cmux_step3's order and barriers (A through X1, then B through X0: X0 is written
+  // only after a barrier that every wave passes after its last X0 read of the body digits).
+  __device__ static __forceinline__ void inv2(double (&xa)[E], double (&xb)[E], double *lds, const double *tw,
+                                              int tid, const double *__restrict__ gt) {
+    int ra = 0, rb = 0;
+    inv_stages<3, 9, 11>(xa, tw, tid, ra);
+    inv_stages<3, 9, 11>(xb, tw, tid, rb);
+    swap23(xa);
+    swap23(xb);
+    inv_stages<2, 6, 9>(xa, tw, tid, ra);
+    inv_stages<2, 6, 9>(xb, tw, tid, rb);
+    exchange_w<2, 1>(xa, lds, tid);
+    exchange_w<2, 1>(xb, lds, tid);
+    inv_stages<1, 3, 6>(xa, tw, tid, ra);
+    inv_stages<1, 3, 6>(xb, tw, tid, rb);
+    exchange_x<1, 0, 1>(xa, lds, tid);
+    exchange_x<1, 0, 0>(xb, lds, tid);
+    inv_stages<0, 0, 3, true>(xa, tw, tid, ra, gt);
+    inv_stages<0, 0, 3, true>(xb, tw, tid, rb, gt);
+  }
   // unscaled inverse (the caller folds N^-1 into the key), tw the forward table (mirrored reads);
   // gt: the same table in global memory (pass-0 twiddles)
   template <int XB>
