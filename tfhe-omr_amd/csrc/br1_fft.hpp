@@ -156,11 +156,11 @@ __device__ __forceinline__ void br1f_step_lds(uint32_t (&ac)[2][16], double2 *xc
   using F = Fft512;
   uint32_t pk[2][16];
   br1f_digits(ac, reinterpret_cast<uint32_t *>(xch), a, lane, pk);
-  double outr[2][1][8], outi[2][1][8];
+  double outr[2][8], outi[2][8];
 #pragma unroll
   for (int o = 0; o < 2; ++o)
 #pragma unroll
-    for (int e = 0; e < 8; ++e) outr[o][0][e] = outi[o][0][e] = 0.0;
+    for (int e = 0; e < 8; ++e) outr[o][e] = outi[o][e] = 0.0;
 #pragma unroll
   for (int p = 0; p < 2; ++p) {
 #pragma unroll 1
@@ -185,21 +185,19 @@ __device__ __forceinline__ void br1f_step_lds(uint32_t (&ac)[2][16], double2 *xc
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const double2 ka = kb[e * 64 + lane], kB = kb[F::N + e * 64 + lane];
-        outr[0][0][e] = __fma_rn(xr[0][e], ka.x, __fma_rn(-xi[0][e], ka.y, outr[0][0][e]));
-        outi[0][0][e] = __fma_rn(xr[0][e], ka.y, __fma_rn(xi[0][e], ka.x, outi[0][0][e]));
-        outr[1][0][e] = __fma_rn(xr[0][e], kB.x, __fma_rn(-xi[0][e], kB.y, outr[1][0][e]));
-        outi[1][0][e] = __fma_rn(xr[0][e], kB.y, __fma_rn(xi[0][e], kB.x, outi[1][0][e]));
+        outr[0][e] = __fma_rn(xr[0][e], ka.x, __fma_rn(-xi[0][e], ka.y, outr[0][e]));
+        outi[0][e] = __fma_rn(xr[0][e], ka.y, __fma_rn(xi[0][e], ka.x, outi[0][e]));
+        outr[1][e] = __fma_rn(xr[0][e], kB.x, __fma_rn(-xi[0][e], kB.y, outr[1][e]));
+        outi[1][e] = __fma_rn(xr[0][e], kB.y, __fma_rn(xi[0][e], kB.x, outi[1][e]));
       }
     }
   }
+  F::inv_pair<true>(outr, outi, xch, tws, lane, gtw);  // both outputs, interleaved
 #pragma unroll
-  for (int o = 0; o < 2; ++o) {
-    F::inv<1, true>(outr[o], outi[o], xch, tws, lane, gtw);
+  for (int o = 0; o < 2; ++o)
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      ac[o][i] = Lvl1Off::add(ac[o][i], Lvl1Int::round_red(i < 8 ? outr[o][0][i] : outi[o][0][i - 8]));
-    }
-  }
+    for (int i = 0; i < 16; ++i)
+      ac[o][i] = Lvl1Off::add(ac[o][i], Lvl1Int::round_red(i < 8 ? outr[o][i] : outi[o][i - 8]));
 }
 
 // Level-1 blind rotations: BR1F_WPG waves per workgroup, one rotation per wave; rotation

@@ -374,6 +374,25 @@ struct WgFft {
     swap01<C>(xr, xi);
     inv8<0, C, G>(xr, xi, tws, lane, gtw);
   }
+  // Two inverses interleaved through ONE transform's exchange buffer: the register passes run on
+  // both (C = 2), the LDS exchange of the second follows the first's in the same slots (one
+  // wave's LDS operations complete in order; the fence keeps the compiler from hoisting the
+  // second's writes above the first's reads).
+  template <bool G = false>
+  __device__ static __forceinline__ void inv_pair(double (&xr)[2][E], double (&xi)[2][E], double2 *lds,
+                                                  const double2 *tws, int lane,
+                                                  const double2 *__restrict__ gtw = nullptr) {
+    inv2<2>(xr, xi, tws, lane);
+    swap23<2>(xr, xi);
+    inv8<2, 2>(xr, xi, tws, lane);
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+      exchange<1, 2, 1>(reinterpret_cast<double(&)[1][E]>(xr[c]), reinterpret_cast<double(&)[1][E]>(xi[c]), lds,
+                        lane);
+    inv4<2>(xr, xi, tws, lane);
+    swap01<2>(xr, xi);
+    inv8<0, 2, G>(xr, xi, tws, lane, gtw);
+  }
   __device__ static __forceinline__ void fwd(double (&xr)[E], double (&xi)[E], double2 *lds,
                                              const double2 *tws, int lane,
                                              const double2 *__restrict__ gtw = nullptr) {
