@@ -156,9 +156,13 @@ const char *omr_detect_kernels(void);
 /* Messages per internal detect chunk (memory/latency knob: 36 KiB of scratch per message);
  * 0 = the default 16,384. */
 omr_status omr_ctx_set_batch(omr_ctx *ctx, size_t batch);
-/* Chunks of at most `max_messages` messages run the latency kernels (each level-1 rotation and
- * each level-2 message spread over more waves: lower single-message latency, bit-identical
- * output); larger chunks run the throughput kernels. Default 64; 0 = always throughput. */
+/* Chunks of at most `max_messages` messages run the latency kernels (each level-1 rotation
+ * spread over more waves, each level-2 message over two CUs that exchange partial products
+ * through global memory every step, or over two wave groups of one CU when 2 x chunk exceeds the
+ * CU count: lower single-message latency, bit-identical output); larger chunks run the
+ * throughput kernels. Default 64; 0 = always throughput. A two-CU exchange that does not
+ * complete (its workgroups not co-resident) ends the kernel and makes the next host-API
+ * omr_detect_batch call return OMR_ERR_DEVICE. */
 omr_status omr_ctx_set_latency_threshold(omr_ctx *ctx, size_t max_messages);
 
 /* Detector::detect (detector.rs:135-166), batched like `par_iter().map(detect)` in
