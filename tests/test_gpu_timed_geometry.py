@@ -1,6 +1,7 @@
 """GPU parity at the geometry bench.py times, through the device entry points.
 
-configs[2] (D = 65,536 in 16,384-message launches) and configs[4]'s per-GPU share (D = 131,072)
+configs[2] (D = 65,536 in one 65,536-message launch, bench.py's default, and in the library's
+default 16,384-message launches) and configs[4]'s per-GPU share (D = 131,072 in two launches)
 run through omr_detect_batch_device on bench.py's seeded keys and clue streams (pack 42 /
 pack 4242, clue seeds 1000 / 1001): every output must pass the omd.rs:48-58 KAT (pertinent ->
 [1, 0, ..., 0], other -> 0) with the library retriever, and the messages at the launch
@@ -54,8 +55,8 @@ def _kat_all(a, d_out, mask, piece=8192):
         assert not dec[:, 1:].any() and not dec[~mask[s:s + piece], 0].any(), f"nonzero slot in [{s}, {s + piece})"
 
 
-@pytest.mark.parametrize("D", [65536, 131072])
-def test_timed_geometry_device_path(ctx, D):
+@pytest.mark.parametrize("D,batch", [(65536, 65536), (65536, 16384), (131072, 65536)])
+def test_timed_geometry_device_path(ctx, D, batch):
     import torch
     a, b, det, orc = ctx
     rng = np.random.default_rng(2025)
@@ -66,7 +67,7 @@ def test_timed_geometry_device_path(ctx, D):
     d_out = torch.empty((D, 2, 2048), dtype=torch.int64, device="cuda:0")
     side = torch.cuda.Stream()
     torch.cuda.synchronize()
-    det.set_batch(16384)  # bench.py's launch size: 4 (8) launches per level
+    det.set_batch(batch)  # bench.py's launch size (65,536) or the library default (16,384)
     with torch.cuda.stream(side):
         det.detect_batch_device(d_ca.data_ptr(), d_cb.data_ptr(), D, d_out.data_ptr(), side.cuda_stream)
     side.synchronize()
