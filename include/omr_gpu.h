@@ -164,6 +164,10 @@ omr_status omr_ctx_set_batch(omr_ctx *ctx, size_t batch);
  * complete (its workgroups not co-resident) ends the kernel and makes the next host-API
  * omr_detect_batch call return OMR_ERR_DEVICE. */
 omr_status omr_ctx_set_latency_threshold(omr_ctx *ctx, size_t max_messages);
+/* Encode workgroups fold ceil(D / max_chunks) messages each (at least 32, or 128 from D = 16,384),
+ * so a call keeps at most `max_chunks` partial digests per ciphertext (32 KiB each); 0 = the
+ * default 4,096. A memory knob: the digests are identical for every setting. */
+omr_status omr_ctx_set_encode_chunks(omr_ctx *ctx, size_t max_chunks);
 
 /* Detector::detect (detector.rs:135-166), batched like `par_iter().map(detect)` in
  * examples/omr.rs:160-164. Host buffers: clue_a u16 [D][512], clue_b u16 [D][7],

@@ -125,6 +125,7 @@ pub mod ffi {
         pub fn omr_detect_kernels() -> *const c_char;
         pub fn omr_ctx_set_batch(ctx: *mut OmrCtx, batch: usize) -> OmrStatus;
         pub fn omr_ctx_set_latency_threshold(ctx: *mut OmrCtx, max_messages: usize) -> OmrStatus;
+        pub fn omr_ctx_set_encode_chunks(ctx: *mut OmrCtx, max_chunks: usize) -> OmrStatus;
         pub fn omr_detect_batch(ctx: *mut OmrCtx, clue_a: *const u16, clue_b: *const u16, d: usize,
                                 out: *mut u64) -> OmrStatus;
         pub fn omr_detect_batch_device(ctx: *mut OmrCtx, d_clue_a: *const u16, d_clue_b: *const u16, d: usize,
@@ -411,6 +412,11 @@ impl GpuDetector {
     /// Messages per internal detect chunk (0 = default).
     pub fn set_batch(&self, batch: usize) -> Result<(), OmrError> {
         check(unsafe { omr_ctx_set_batch(self.ctx, batch) })
+    }
+
+    /// At most `max_chunks` partial digests per encode ciphertext (0 = default 4,096).
+    pub fn set_encode_chunks(&self, max_chunks: usize) -> Result<(), OmrError> {
+        check(unsafe { omr_ctx_set_encode_chunks(self.ctx, max_chunks) })
     }
 
     /// Chunks of at most `max_messages` messages run the latency kernels (0 = never).

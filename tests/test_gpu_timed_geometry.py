@@ -112,12 +112,16 @@ def test_device_calls_on_two_streams_and_host_call(ctx):
         assert np.array_equal(got[k], orc.detect_batch(ca, cb, nthreads=THREADS)), f"call {k}"
 
 
-def test_encode_device_large_multi_ct(ctx):
+@pytest.mark.parametrize("max_chunks", [0, 7])
+def test_encode_device_large_multi_ct(ctx, max_chunks):
     """encode_*_device at D = 20,000 (the 128-message-per-workgroup path), 5 index ciphertexts
     and 3 payload ciphertexts of 2 combinations, global offset 12,345 of a 100,000 board, on a
-    side stream; bit-exact against the oracle and against the host entry points."""
+    side stream; bit-exact against the oracle and against the host entry points. max_chunks = 7
+    gives 2,858 messages per workgroup, the regime of D > 524,288 at the default 4,096 chunks
+    (the index kernel stages its bucket choices 128 messages at a time)."""
     import torch
     _, _, det, _ = ctx
+    det.set_encode_chunks(max_chunks)
     D, off, allc = 20000, 12345, 100000
     rng = np.random.default_rng(5)
     pv = rng.integers(0, A.Q2, (D, 2, 2048), dtype=np.uint64)
@@ -144,6 +148,7 @@ def test_encode_device_large_multi_ct(ctx):
     assert np.array_equal(idx[2], det.encode_pertinent_indices(rp, pv, 9, 2, global_offset=off))
     assert np.array_equal(dig, O.encode_payloads(pv, pay, off, allc, w, n_pay, per))
     assert np.array_equal(dig, det.encode_pertinent_payloads(pv, pay, w, rp, global_offset=off))
+    det.set_encode_chunks(0)
 
 
 def test_encode_rejects_bad_shapes(ctx):

@@ -134,6 +134,7 @@ struct omr_ctx {
   uint16_t *trace_tabs = nullptr;
   DeviceTables tb{};
   size_t batch = OMR_DEFAULT_BATCH, batch_cap = 0;
+  size_t enc_max_chunks = OMR_ENC_MAX_CHUNKS;  // chunk partials per encode ciphertext (omr_ctx_set_encode_chunks)
   uint32_t *ext = nullptr, *lwe1t = nullptr, *lwe_int = nullptr;
   // chunks of at most latency_max messages run the latency kernels (latency_kernels.hpp)
   size_t latency_max = OMR_DEFAULT_LATENCY_MAX;
@@ -531,6 +532,13 @@ extern "C" omr_status omr_ctx_set_batch(omr_ctx *c, size_t batch) {
   return ensure_batch(c, c->batch);
 }
 
+extern "C" omr_status omr_ctx_set_encode_chunks(omr_ctx *c, size_t max_chunks) {
+  if (!c) return set_error(OMR_ERR_INVALID_ARGUMENT, "omr_ctx_set_encode_chunks: NULL ctx");
+  std::lock_guard<std::mutex> lk(c->mu);
+  c->enc_max_chunks = max_chunks ? max_chunks : OMR_ENC_MAX_CHUNKS;
+  return OMR_OK;
+}
+
 extern "C" omr_status omr_ctx_set_latency_threshold(omr_ctx *c, size_t max_messages) {
   if (!c) return set_error(OMR_ERR_INVALID_ARGUMENT, "omr_ctx_set_latency_threshold: NULL ctx");
   std::lock_guard<std::mutex> lk(c->mu);
@@ -685,11 +693,12 @@ extern "C" omr_status omr_last_timing(omr_ctx *c, omr_detect_timing *t) {
 // Encode (detector.rs:223-453)
 // ------------------------------------------------------------------------------------------
 namespace {
-// Messages per encode workgroup: at least 32 (128 from D = 16,384), and at most 4,096 chunk
-// partials per ciphertext (scratch n_ct x chunks x 32 KiB: 3.7 GB for 28 ciphertexts at D = 2^20).
-int encode_per_wg(size_t D) {
+// Messages per encode workgroup: at least 32 (128 from D = 16,384), and at most max_chunks
+// (default 4,096) chunk partials per ciphertext (scratch n_ct x chunks x 32 KiB: 3.7 GB for 28
+// ciphertexts at D = 2^20); above ENC_T messages the index kernel stages its buckets in blocks.
+int encode_per_wg(size_t D, size_t max_chunks) {
   const size_t base = D >= 16384 ? 128 : 32;
-  return (int)std::max(base, (D + 4095) / 4096);
+  return (int)std::max(base, (D + max_chunks - 1) / max_chunks);
 }
 }  // namespace
 
@@ -709,7 +718,7 @@ extern "C" omr_status omr_encode_indices_device(omr_ctx *c, const uint64_t *pv, 
     HIP_TRY(hipMemsetAsync(out, 0, (size_t)n_ct * 2 * N2 * sizeof(uint64_t), st));
     return OMR_OK;
   }
-  const int per_wg = encode_per_wg(D);
+  const int per_wg = encode_per_wg(D, c->enc_max_chunks);
   const int chunks = (int)((D + per_wg - 1) / per_wg);
   if ((s = ensure_partial(c, (size_t)n_ct * chunks * 2 * N2)) != OMR_OK) return s;
   if ((s = scratch_acquire(c, st)) != OMR_OK) return s;
@@ -738,7 +747,7 @@ extern "C" omr_status omr_encode_payloads_device(omr_ctx *c, const uint64_t *pv,
     HIP_TRY(hipMemsetAsync(out, 0, (size_t)n_ct * 2 * N2 * sizeof(uint64_t), st));
     return OMR_OK;
   }
-  const int per_wg = encode_per_wg(D);
+  const int per_wg = encode_per_wg(D, c->enc_max_chunks);
   const int chunks = (int)((D + per_wg - 1) / per_wg);
   omr_status s;
   if ((s = ensure_partial(c, (size_t)n_ct * chunks * 2 * N2)) != OMR_OK) return s;

@@ -31,47 +31,53 @@ __global__ __launch_bounds__(ENC_T) void encode_indices_kernel(
   const uint32_t ct = first_ct + cti;
   const int m0 = chunk * per_wg;
   const int mcount = min(per_wg, D - m0);
-  if (tid < mcount) {
-    uint32_t w[16];
-    bucket_words(seed, ct, offset + m0 + tid, w);
-    for (int s = 0; s < ly.segment_per_cipher && s < 8; ++s) buckets[tid][s] = (uint8_t)bucket_of(w[s]);
-  }
-  __syncthreads();
   double accA[E], accB[E];
 #pragma unroll
   for (int e = 0; e < E; ++e) accA[e] = accB[e] = 0.0;
+  // per_wg may exceed ENC_T (large D): the bucket choices are staged ENC_T messages at a time
 #pragma unroll 1
-  for (int mi = 0; mi < mcount; ++mi) {
-    const uint64_t gi = offset + m0 + mi;
-    double x[E];
+  for (int mb = 0; mb < mcount; mb += ENC_T) {
+    const int cnt = min(ENC_T, mcount - mb);
+    __syncthreads();  // every thread has finished reading the previous block's buckets
+    if (tid < cnt) {
+      uint32_t w[16];
+      bucket_words(seed, ct, offset + m0 + mb + tid, w);
+      for (int s = 0; s < ly.segment_per_cipher && s < 8; ++s) buckets[tid][s] = (uint8_t)bucket_of(w[s]);
+    }
+    __syncthreads();
+#pragma unroll 1
+    for (int mi = mb; mi < mb + cnt; ++mi) {
+      const uint64_t gi = offset + m0 + mi;
+      double x[E];
 #pragma unroll
-    for (int e = 0; e < E; ++e) {
-      const int pos = tid + e * T;
-      const int s = pos / ly.slots_per_segment;
-      double v = 0.0;
-      if (s < ly.segment_per_cipher) {
-        const int within = pos - s * ly.slots_per_segment;
-        const int bk = within / ly.slots_per_bucket;
-        const int slot = within - bk * ly.slots_per_bucket;
-        if (bk == buckets[mi][s]) {
-          if (slot == ly.index_slots) {
-            v = 1.0;
-          } else {
-            uint64_t t = gi;  // base-257 digit `slot` of gi (little endian)
-            for (int q = 0; q < slot; ++q) t /= (uint64_t)P;
-            v = centred_lift((uint32_t)(t % (uint64_t)P));
+      for (int e = 0; e < E; ++e) {
+        const int pos = tid + e * T;
+        const int s = pos / ly.slots_per_segment;
+        double v = 0.0;
+        if (s < ly.segment_per_cipher) {
+          const int within = pos - s * ly.slots_per_segment;
+          const int bk = within / ly.slots_per_bucket;
+          const int slot = within - bk * ly.slots_per_bucket;
+          if (bk == buckets[mi - mb][s]) {
+            if (slot == ly.index_slots) {
+              v = 1.0;
+            } else {
+              uint64_t t = gi;  // base-257 digit `slot` of gi (little endian)
+              for (int q = 0; q < slot; ++q) t /= (uint64_t)P;
+              v = centred_lift((uint32_t)(t % (uint64_t)P));
+            }
           }
         }
+        x[e] = v;
       }
-      x[e] = v;
-    }
-    NTT::fwd(x, xch, tw, tid);
-    const uint64_t *pa = pv + (size_t)(m0 + mi) * 2 * N + tid * E;
-    const uint64_t *pb = pa + N;
+      NTT::fwd(x, xch, tw, tid);
+      const uint64_t *pa = pv + (size_t)(m0 + mi) * 2 * N + tid * E;
+      const uint64_t *pb = pa + N;
 #pragma unroll
-    for (int e = 0; e < E; ++e) {
-      accA[e] = red<M>(accA[e] + mm<M>(from_u64<M>(pa[e]), x[e]));
-      accB[e] = red<M>(accB[e] + mm<M>(from_u64<M>(pb[e]), x[e]));
+      for (int e = 0; e < E; ++e) {
+        accA[e] = red<M>(accA[e] + mm<M>(from_u64<M>(pa[e]), x[e]));
+        accB[e] = red<M>(accB[e] + mm<M>(from_u64<M>(pb[e]), x[e]));
+      }
     }
   }
   uint64_t *o = partial + ((size_t)cti * gridDim.x + chunk) * 2 * N + tid * E;

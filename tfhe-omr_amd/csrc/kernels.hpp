@@ -15,6 +15,7 @@ constexpr int BR2_T = 256, BR2_E = 8;  // N2 = 2048
 constexpr int BR2_WAVES = 2;
 constexpr int ENC_T = 128, ENC_E = 16;
 constexpr size_t OMR_DEFAULT_BATCH = 16384;  // messages per detect chunk (scratch 36 KiB/msg)
+constexpr size_t OMR_ENC_MAX_CHUNKS = 4096;   // default chunk partials per encode ciphertext
 
 struct DeviceTables {
   const double *tw1, *itw1, *tw2, *itw2;  // psi^brv(k), psi^-brv(k) (centred)

@@ -69,6 +69,7 @@ EXPORTS = {
     "omr_ctx_destroy": (None, [C.c_void_p]),
     "omr_ctx_set_batch": (C.c_int, [C.c_void_p, C.c_size_t]),
     "omr_ctx_set_latency_threshold": (C.c_int, [C.c_void_p, C.c_size_t]),
+    "omr_ctx_set_encode_chunks": (C.c_int, [C.c_void_p, C.c_size_t]),
     "omr_detect_batch": (C.c_int, [C.c_void_p, _u16p, _u16p, C.c_size_t, _u64p]),
     "omr_detect_batch_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p]),
     "omr_ctx_enable_timing": (C.c_int, [C.c_void_p, C.c_int]),
@@ -382,6 +383,10 @@ class Detector:
 
     def set_batch(self, batch: int):
         _check(lib().omr_ctx_set_batch(self._h, batch), "omr_ctx_set_batch")
+
+    def set_encode_chunks(self, max_chunks: int):
+        """At most max_chunks partial digests per encode ciphertext (0 = default 4,096)."""
+        _check(lib().omr_ctx_set_encode_chunks(self._h, max_chunks), "omr_ctx_set_encode_chunks")
 
     def set_latency_threshold(self, max_messages: int):
         """Chunks of at most max_messages messages use the latency kernels (0: never)."""
