@@ -5,9 +5,9 @@
 // one wave (workgroup) while the rest of the chip idles: 9 + 16.6 ms of its 27 ms latency.
 // Here every CMUX step's digit transforms are split over more waves, whose partial
 // multiply-accumulates are summed through LDS before the inverse transforms:
-//   level 1 (br1l_kernel): one 4-wave workgroup per rotation; wave w transforms mask digit w and
-//     body digit w (2 FFTs instead of 8), waves 0 / 1 sum the partials of output A / B, run its
-//     inverse FFT and own the mask / body accumulator;
+//   level 1 (br1l_kernel): one 8-wave workgroup per rotation; wave w transforms one of the 8
+//     digit polynomials (1 FFT instead of 8) and adds its products into the two output sums in
+//     LDS, waves 0 / 1 run the inverse FFT of output A / B and own the mask / body accumulator;
 //   level 2 (br2l_kernel): one 8-wave workgroup per message, two groups of four waves; group 0
 //     transforms the 6 mask digits, group 1 the 6 body digits, each sums one output and runs one
 //     inverse NTT (6 + 1 transforms per group instead of 12 + 2); the trace runs after it
@@ -23,7 +23,15 @@
 namespace omr {
 
 // ---- level 1 ---------------------------------------------------------------------------------
-constexpr int BR1L_WAVES = D1;  // one wave per gadget digit (mask and body digit w)
+// Level 1 over eight waves (one GGSW row each: wave w = p * D1 + k transforms digit k of
+// polynomial p, p = 0 mask, 1 body): each wave extracts one digit (16 coefficients instead of 32),
+// runs one forward FFT instead of two interleaved ones, and adds its products into the two output
+// sums in LDS with ds_add_f64 (the FFT product rounds to the exact integer whatever the summation
+// order, device_fft.hpp), so the partials need 16 KB instead of 64 KB. Waves 0 / 1 then read and
+// clear sum A / B, run its inverse and own the mask / body accumulator. Single-message level 1
+// 3.8 ms against 4.5 ms for four waves with two interleaved transforms each and partials summed
+// from LDS (profiles/r02j/latency_br1l_8wave_ab.log).
+constexpr int BR1L_WAVES = 2 * D1;
 
 __global__ __launch_bounds__(64 * BR1L_WAVES, 1) void br1l_kernel(
     const uint16_t *__restrict__ clue_a, const uint16_t *__restrict__ clue_b,
@@ -32,12 +40,13 @@ __global__ __launch_bounds__(64 * BR1L_WAVES, 1) void br1l_kernel(
     uint64_t *__restrict__ rlwe_out, int mode) {
   using F = Fft512;
   constexpr int NF = F::N, W = BR1L_WAVES;
-  __shared__ int ext[2][2 * N1];               // [ACC, -ACC] per poly (0 mask, 1 body)
-  __shared__ double2 xch_all[W][2 * F::BUF];   // per wave: two interleaved transforms
-  __shared__ double2 part[W][2][8 * 64];       // partial outputs A, B: slot e * 64 + lane
+  __shared__ int ext[2][2 * N1];              // [ACC, -ACC] per poly (0 mask, 1 body)
+  __shared__ double2 xch_all[W][F::BUF];      // per wave: one transform
+  __shared__ double sum[2][2][8 * 64];        // outputs A, B: [re, im][slot e * 64 + lane]
   __shared__ double2 tws[NF];
   __shared__ uint16_t la[N0];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int p = wave / D1, k = wave % D1;
   double2 *xch = xch_all[wave];
   const size_t g = blockIdx.x;  // rotation
   int b;
@@ -66,71 +75,50 @@ __global__ __launch_bounds__(64 * BR1L_WAVES, 1) void br1l_kernel(
     }
   }
   for (int j = threadIdx.x; j < NF; j += 64 * W) tws[j] = tb.fft1[j];
+  for (int j = threadIdx.x; j < 2 * 2 * 8 * 64; j += 64 * W) (&sum[0][0][0])[j] = 0.0;
   __syncthreads();
 #pragma unroll 1
   for (int i = 0; i < N0; ++i) {
     const int a = __builtin_amdgcn_readfirstlane(la[i]);
     if (a == 0) continue;  // (X^0 - 1) * ACC = 0 (a is uniform over the workgroup)
-    // GGSW rows of this wave: mask digit `wave` (row wave) and body digit `wave` (row D1 + wave)
-    const double2 *km = bskf + ((size_t)i * 2 * D1 + wave) * 2 * NF + lane * 8;
-    const double2 *kb = bskf + ((size_t)i * 2 * D1 + D1 + wave) * 2 * NF + lane * 8;
-    double2 k[2][2][8];  // [digit row mask/body][output A/B][point]
+    const double2 *kr = bskf + ((size_t)i * 2 * D1 + wave) * 2 * NF + lane * 8;  // GGSW row `wave`
+    double2 kk[2][8];  // [output A/B][point]
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      k[0][0][e] = km[e];
-      k[0][1][e] = km[NF + e];
-      k[1][0][e] = kb[e];
-      k[1][1][e] = kb[NF + e];
+      kk[0][e] = kr[e];
+      kk[1][e] = kr[NF + e];
     }
-    // digit `wave` of (X^a - 1) * ACC_p for both polys (the shared [ACC, -ACC] extensions)
-    double xr[2][8], xi[2][8];
+    double xr[1][8], xi[1][8];
     const int base = lane - a + 2 * N1;
 #pragma unroll
-    for (int p = 0; p < 2; ++p)
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int j = acc_coef(lane, q);
-        const uint32_t w = Lvl1Int::digits(
-            Lvl1Int::canon(ext[p][(base + acc_coef(0, q)) & (2 * N1 - 1)] - ext[p][j]));
-        const double d = Lvl1Int::digit_shifts(w, wave);
-        if (q < 8)
-          xr[p][q] = d;
-        else
-          xi[p][q - 8] = d;
-      }
-    F::fwd<2, true>(xr, xi, xch, tws, lane, tb.fft1);
-    double2 o[2][8];
+    for (int q = 0; q < 16; ++q) {
+      const int j = acc_coef(lane, q);
+      const uint32_t w = Lvl1Int::digits(Lvl1Int::canon(ext[p][(base + acc_coef(0, q)) & (2 * N1 - 1)] - ext[p][j]));
+      const double d = Lvl1Int::digit_shifts(w, k);
+      if (q < 8)
+        xr[0][q] = d;
+      else
+        xi[0][q - 8] = d;
+    }
+    F::fwd<1, true>(xr, xi, xch, tws, lane, tb.fft1);
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        double re = 0.0, im = 0.0;
-#pragma unroll
-        for (int p = 0; p < 2; ++p) {
-          re = __fma_rn(xr[p][e], k[p][t][e].x, __fma_rn(-xi[p][e], k[p][t][e].y, re));
-          im = __fma_rn(xr[p][e], k[p][t][e].y, __fma_rn(xi[p][e], k[p][t][e].x, im));
-        }
-        o[t][e] = make_double2(re, im);
+        const double re = __fma_rn(xr[0][e], kk[t][e].x, -xi[0][e] * kk[t][e].y);
+        const double im = __fma_rn(xr[0][e], kk[t][e].y, xi[0][e] * kk[t][e].x);
+        __hip_atomic_fetch_add(&sum[t][0][e * 64 + lane], re, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_fetch_add(&sum[t][1][e * 64 + lane], im, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) part[wave][t][e * 64 + lane] = o[t][e];
     __syncthreads();
-    if (wave < 2) {  // wave 0: output A (mask accumulator), wave 1: output B (body accumulator).
-      // The FFT product is exact after rounding whatever the summation order (device_fft.hpp).
+    if (wave < 2) {  // wave 0: output A (mask accumulator), wave 1: output B (body accumulator)
       double sr[1][8], si[1][8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        double2 s = part[0][wave][e * 64 + lane];
-#pragma unroll
-        for (int w = 1; w < W; ++w) {
-          const double2 v = part[w][wave][e * 64 + lane];
-          s.x += v.x;
-          s.y += v.y;
-        }
-        sr[0][e] = s.x;
-        si[0][e] = s.y;
+        sr[0][e] = sum[wave][0][e * 64 + lane];
+        si[0][e] = sum[wave][1][e * 64 + lane];
+        sum[wave][0][e * 64 + lane] = 0.0;  // cleared for the next step (after the barrier below)
+        sum[wave][1][e * 64 + lane] = 0.0;
       }
       F::inv<1, true>(sr, si, xch, tws, lane, tb.fft1);
 #pragma unroll
