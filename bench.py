@@ -260,8 +260,8 @@ def main():
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
-    det.enable_timing(True)
-    stage = {"first_level_ms": 0.0, "key_switch_ms": 0.0, "second_level_ms": 0.0}
+    det.enable_timing(1)  # stage events around the production kernels (trace fused into level 2)
+    stage = {"first_level_ms": 0.0, "key_switch_ms": 0.0, "second_level_ms": 0.0, "trace_ms": 0.0}
     start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize(dev)
     t = time.perf_counter()
@@ -277,13 +277,29 @@ def main():
     if dist:
         dist.barrier()
     wall = time.perf_counter() - t
-    det.enable_timing(False)
+    backend.synchronize()  # raises if a detect call failed on the device
     gpu_ms = start.elapsed_time(end)
     elapsed = max(wall, gpu_ms / 1e3)
     if dist:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
+
+    # Detector::detect_with_time_info's split (detector.rs:169-221) on one untimed pass: timing
+    # mode 2 runs the level-2 rotation and the trace as two launches, so the trace gets its own time
+    det.enable_timing(2)
+    backend.detect(d_ca, d_cb, out=d_out)
+    split = det.last_timing()
+    det.enable_timing(0)
+    backend.synchronize()
+    time_info = {"total_detect_ms": round(split["total_ms"], 2),
+                 "first_level_bootstrapping_ms": round(split["first_level_ms"], 2),
+                 "second_level_bootstrapping_ms": round(split["second_level_ms"], 2),
+                 "trace_ms": round(split["trace_ms"], 2),
+                 "key_switch_ms": round(split["key_switch_ms"], 2), "messages": int(split["messages"]),
+                 "trace_separate": bool(split["trace_separate"]),
+                 "note": "one untimed detect pass in timing mode 2 (trace as its own launch); DetectTimeInfo "
+                         "fields (detector.rs:51-57), first level includes the key switch"}
 
     # correctness spot check on this rank's data: the client decrypts (library Retriever, CPU)
     # and every pertinency ciphertext must decode to [1, 0, ..., 0] or all zeros (omd.rs:48-58)
@@ -325,6 +341,9 @@ def main():
                 det.detect_batch_device(d_ca.data_ptr(), d_cb.data_ptr(), 1, one_out.data_ptr(), stream.cuda_stream)
                 torch.cuda.synchronize(dev)
                 lat.append((time.perf_counter() - t1) * 1e3)
+                det.check(stream.cuda_stream)  # raises on a failed two-CU hand-off
+                if not torch.equal(one_out[0], d_out[0]):  # same message as the timed throughput pass
+                    raise RuntimeError("single-message detect differs from the throughput kernels' output")
             return round(min(lat), 3)
 
         latency_ms = one_message()
@@ -340,7 +359,8 @@ def main():
     msgs = args.steps * total
     value = msgs / elapsed
     names = A.detect_kernels()
-    kms = {"br1": stage["first_level_ms"], "ks": stage["key_switch_ms"], "br2": stage["second_level_ms"]}
+    kms = {"br1": stage["first_level_ms"] - stage["key_switch_ms"], "ks": stage["key_switch_ms"],
+           "br2": stage["second_level_ms"] + stage["trace_ms"]}
     role = max(kms, key=kms.get)
     chunks = -(-D // args.batch)
     roof, hbm = rooflines(role, names[role], args.steps * chunks, D / chunks, kms[role], value, world)
@@ -364,7 +384,11 @@ def main():
                    "pertinent": int(len(pert)), "batch": args.batch, "parallelism": f"dp{world}"},
         "latency_ms_per_message": latency_ms,
         "latency_ms_per_message_throughput_kernels": latency_tp_ms,
-        "stage_ms_per_step": {k: round(v / args.steps, 2) for k, v in stage.items()},
+        "stage_ms_per_step": dict({k: round(v / args.steps, 2) for k, v in stage.items()},
+                                  note="timed steps, timing mode 1: first_level includes the key switch; "
+                                       "the throughput kernel fuses the trace into second_level (trace_ms 0); "
+                                       "split: detect_time_info"),
+        "detect_time_info": time_info,
         "detect_bytes_per_message": DETECT_BYTES,
         "roofline": roof,
         "hbm": hbm,

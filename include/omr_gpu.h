@@ -128,9 +128,12 @@ omr_status omr_retrieve_indices(const omr_secret_key_pack *sk, const uint64_t *i
 /* decode_combined_payloads + solve_matrix_mod_257 (retriever.rs:203-258, matrix.rs:164-247):
  * payloads u16 [n_indices][612] of the sorted retrieved indices, from the payload digest
  * ciphertexts and the board's weights (omr_payload_weights, same seed as the detector).
- * OMR_ERR_NOT_INVERTIBLE when the system is singular. */
+ * `combination_count` is the board's RetrievalParams::combination_count (the reference's matrix
+ * has that many rows whatever the number of indices found, retriever.rs:196, :215-239); 0 takes
+ * the count of a board whose pertinent count is n_indices. OMR_ERR_NOT_INVERTIBLE when the system
+ * is singular. */
 omr_status omr_retrieve_payloads(const omr_secret_key_pack *sk, const uint64_t *pay_cts,
-                                 uint32_t n_ct, size_t all_payloads_count,
+                                 uint32_t n_ct, size_t all_payloads_count, uint32_t combination_count,
                                  const uint16_t *weights, const size_t *indices, size_t n_indices,
                                  uint16_t *payloads);
 
@@ -158,12 +161,19 @@ const char *omr_detect_kernels(void);
 omr_status omr_ctx_set_batch(omr_ctx *ctx, size_t batch);
 /* Chunks of at most `max_messages` messages run the latency kernels (each level-1 rotation
  * spread over more waves, each level-2 message over two CUs that exchange partial products
- * through global memory every step, or over two wave groups of one CU when 2 x chunk exceeds the
- * CU count: lower single-message latency, bit-identical output); larger chunks run the
- * throughput kernels. Default 64; 0 = always throughput. A two-CU exchange that does not
- * complete (its workgroups not co-resident) ends the kernel and makes the next host-API
- * omr_detect_batch call return OMR_ERR_DEVICE. */
+ * through global memory every step, or over two wave groups of one CU when the cooperative
+ * launch of the two-CU grid is refused: lower single-message latency, bit-identical output);
+ * larger chunks run the throughput kernels. Default 64; 0 = always throughput. The two-CU grid
+ * is launched with hipLaunchCooperativeKernel, so its workgroups are co-resident; if a hand-off
+ * still does not complete, the kernel ends, its output is invalid and the error is reported by
+ * omr_ctx_check (after the caller's stream sync), by the host entry points, and by the next
+ * detect call on the context (which then returns OMR_ERR_DEVICE without running). */
 omr_status omr_ctx_set_latency_threshold(omr_ctx *ctx, size_t max_messages);
+/* Synchronises `hip_stream` (NULL: the whole device) and reports a pending device-side
+ * failure of an earlier call on the context (the two-CU hand-off timeout above) as
+ * OMR_ERR_DEVICE, clearing it; OMR_OK when every call completed correctly. Callers of the
+ * device entry points use it where they would otherwise only synchronise. */
+omr_status omr_ctx_check(omr_ctx *ctx, void *hip_stream);
 /* Encode workgroups fold ceil(D / max_chunks) messages each (at least 32, or 128 from D = 16,384),
  * so a call keeps at most `max_chunks` partial digests per ciphertext (32 KiB each); 0 = the
  * default 4,096. A memory knob: the digests are identical for every setting. */
@@ -174,22 +184,38 @@ omr_status omr_ctx_set_encode_chunks(omr_ctx *ctx, size_t max_chunks);
  * out u64 [D][2][2048] (NTT domain). */
 omr_status omr_detect_batch(omr_ctx *ctx, const uint16_t *clue_a, const uint16_t *clue_b,
                             size_t D, uint64_t *out);
-/* Same on device buffers, enqueued on `hip_stream` (NULL = the context's stream);
- * returns once enqueued. Calls on one context may use different streams: they share the
+/* Same on device buffers, enqueued on `hip_stream` (NULL = HIP's null stream, which orders with
+ * the other blocking streams, as in every HIP API); returns once enqueued. Calls on one context may use different streams: they share the
  * context's scratch, so a call's kernels wait (hipStreamWaitEvent) for those of the previous
  * call on another stream; the caller orders its own buffers. */
 omr_status omr_detect_batch_device(omr_ctx *ctx, const uint16_t *d_clue_a,
                                    const uint16_t *d_clue_b, size_t D, uint64_t *d_out,
                                    void *hip_stream);
 
-/* Detector::detect_with_time_info (detector.rs:169-221): device time of the last detect call
- * per stage, milliseconds (recorded only when enabled; enabling adds events per stage). */
+/* Detector::detect_with_time_info (detector.rs:169-221): device time per stage of the last detect
+ * call, milliseconds, summed over its messages like DetectTimeInfo (detector.rs:51-57):
+ *   total_ms        total_detect_time                      = first_level + second_level + trace
+ *   first_level_ms  total_first_level_bootstrapping_time   7 rotations + sum + key switch + mod switch
+ *   second_level_ms total_second_level_bootstrapping_time  level-2 blind rotation
+ *   trace_ms        total_trace_time                       hom_trace + NTT
+ *   key_switch_ms   the sum + key-switch + mod-switch part of first_level_ms (two_level_bs.rs:62-73)
+ * Timing modes (omr_ctx_enable_timing): 0 off; 1 stage events around the production kernels —
+ * the throughput path fuses the trace into the level-2 kernel, so there trace_ms is 0,
+ * second_level_ms includes it and trace_separate is 0; 2 the reference's split: the throughput
+ * path runs the level-2 rotation and the trace as two launches (same output, slightly slower),
+ * trace_separate = 1. The latency kernels always run the trace as its own launch. */
 typedef struct {
-  float total_ms, first_level_ms, key_switch_ms, second_level_ms; /* second_level includes trace */
+  float total_ms, first_level_ms, second_level_ms, trace_ms, key_switch_ms;
   size_t messages;
+  int trace_separate;
 } omr_detect_timing;
-omr_status omr_ctx_enable_timing(omr_ctx *ctx, int enable);
+omr_status omr_ctx_enable_timing(omr_ctx *ctx, int mode);
 omr_status omr_last_timing(omr_ctx *ctx, omr_detect_timing *t);
+/* omr_detect_batch in timing mode 2 and omr_last_timing as one call under the context's lock
+ * (concurrent callers cannot switch timing off under each other or read another call's times);
+ * the context's timing mode is left as it was. */
+omr_status omr_detect_with_time_info(omr_ctx *ctx, const uint16_t *clue_a, const uint16_t *clue_b,
+                                     size_t D, uint64_t *out, omr_detect_timing *t);
 
 /* Detector::encode_pertinent_indices (detector.rs:223-339) for index ciphertext `ct` over the
  * messages with global indices [global_offset, global_offset+D) of an all_payloads_count board.

@@ -20,6 +20,7 @@
 use std::ffi::CStr;
 use std::fmt;
 use std::os::raw::{c_char, c_int, c_void};
+use std::time::Duration;
 
 /// Raw bindings of `include/omr_gpu.h`, one declaration per C entry point.
 pub mod ffi {
@@ -80,9 +81,11 @@ pub mod ffi {
     pub struct OmrDetectTiming {
         pub total_ms: f32,
         pub first_level_ms: f32,
-        pub key_switch_ms: f32,
         pub second_level_ms: f32,
+        pub trace_ms: f32,
+        pub key_switch_ms: f32,
         pub messages: usize,
+        pub trace_separate: c_int,
     }
 
     extern "C" {
@@ -116,7 +119,8 @@ pub mod ffi {
                                     all_payloads_count: usize, pertinent_count: usize, indices: *mut usize,
                                     cap: usize, found: *mut usize) -> OmrStatus;
         pub fn omr_retrieve_payloads(sk: *const OmrSecretKeyPack, pay_cts: *const u64, n_ct: u32,
-                                     all_payloads_count: usize, weights: *const u16, indices: *const usize,
+                                     all_payloads_count: usize, combination_count: u32, weights: *const u16,
+                                     indices: *const usize,
                                      n_indices: usize, payloads: *mut u16) -> OmrStatus;
 
         // detector (detector.rs:85-453)
@@ -130,8 +134,11 @@ pub mod ffi {
                                 out: *mut u64) -> OmrStatus;
         pub fn omr_detect_batch_device(ctx: *mut OmrCtx, d_clue_a: *const u16, d_clue_b: *const u16, d: usize,
                                        d_out: *mut u64, hip_stream: *mut c_void) -> OmrStatus;
-        pub fn omr_ctx_enable_timing(ctx: *mut OmrCtx, enable: c_int) -> OmrStatus;
+        pub fn omr_ctx_enable_timing(ctx: *mut OmrCtx, mode: c_int) -> OmrStatus;
         pub fn omr_last_timing(ctx: *mut OmrCtx, t: *mut OmrDetectTiming) -> OmrStatus;
+        pub fn omr_detect_with_time_info(ctx: *mut OmrCtx, clue_a: *const u16, clue_b: *const u16, d: usize,
+                                         out: *mut u64, t: *mut OmrDetectTiming) -> OmrStatus;
+        pub fn omr_ctx_check(ctx: *mut OmrCtx, hip_stream: *mut c_void) -> OmrStatus;
         pub fn omr_encode_indices(ctx: *mut OmrCtx, pv: *const u64, d: usize, global_offset: usize,
                                   all_payloads_count: usize, seed: u64, ct: u32, out: *mut u64) -> OmrStatus;
         pub fn omr_encode_indices_device(ctx: *mut OmrCtx, d_pv: *const u64, d: usize, global_offset: usize,
@@ -312,8 +319,29 @@ impl Drop for SecretKeyPack {
     }
 }
 
-/// `DetectTimeInfo` (detector.rs:41-80): device time per stage of the last detect call.
-pub type DetectTimeInfo = OmrDetectTiming;
+/// `DetectTimeInfo` (detector.rs:51-57): summed device time per stage of a detect batch.
+#[derive(Debug, Clone, Copy, Default)]
+pub struct DetectTimeInfo {
+    pub total_detect_time: Duration,
+    /// 7 level-1 rotations + sum + key switch + modulus switch (detector.rs:183-189)
+    pub total_first_level_bootstrapping_time: Duration,
+    /// level-2 blind rotation (detector.rs:193-198)
+    pub total_second_level_bootstrapping_time: Duration,
+    /// hom_trace + NTT (detector.rs:202-209)
+    pub total_trace_time: Duration,
+}
+
+impl From<OmrDetectTiming> for DetectTimeInfo {
+    fn from(t: OmrDetectTiming) -> Self {
+        let ms = |v: f32| Duration::from_secs_f64(f64::from(v.max(0.0)) * 1e-3);
+        Self {
+            total_detect_time: ms(t.total_ms),
+            total_first_level_bootstrapping_time: ms(t.first_level_ms),
+            total_second_level_bootstrapping_time: ms(t.second_level_ms),
+            total_trace_time: ms(t.trace_ms),
+        }
+    }
+}
 
 /// `Detector` on one MI355X: owns the device-resident evaluation keys.
 pub struct GpuDetector {
@@ -357,16 +385,26 @@ impl GpuDetector {
         Ok(out.chunks_exact(2 * OMR_N2).map(NttRlwe::from_flat).collect())
     }
 
-    /// `Detector::detect_with_time_info` (detector.rs:169-221) over a batch.
+    /// `Detector::detect_with_time_info` (detector.rs:169-221) over a batch: detect and the stage
+    /// times in one call under the context's lock (safe with concurrent callers).
     pub fn detect_with_time_info(&self, clues: &[Clue]) -> Result<(Vec<NttRlwe>, DetectTimeInfo), OmrError> {
-        check(unsafe { omr_ctx_enable_timing(self.ctx, 1) })?;
-        let res = self.detect_batch(clues);
+        let d = clues.len();
+        let mut a = Vec::with_capacity(d * OMR_N0);
+        let mut b = Vec::with_capacity(d * OMR_CLUE_COUNT);
+        for c in clues {
+            a.extend_from_slice(&c.a);
+            b.extend_from_slice(&c.b);
+        }
+        let mut out = vec![0u64; d * 2 * OMR_N2];
         let mut t = OmrDetectTiming::default();
-        let st = unsafe { omr_last_timing(self.ctx, &mut t) };
-        check(unsafe { omr_ctx_enable_timing(self.ctx, 0) })?;
-        let out = res?;
-        check(st)?;
-        Ok((out, t))
+        check(unsafe { omr_detect_with_time_info(self.ctx, a.as_ptr(), b.as_ptr(), d, out.as_mut_ptr(), &mut t) })?;
+        Ok((out.chunks_exact(2 * OMR_N2).map(NttRlwe::from_flat).collect(), t.into()))
+    }
+
+    /// Waits for `hip_stream` (null = the whole device) and reports a failed earlier device
+    /// call on this context (`omr_ctx_check`); callers of the device entry points use it.
+    pub fn check(&self, hip_stream: *mut c_void) -> Result<(), OmrError> {
+        check(unsafe { omr_ctx_check(self.ctx, hip_stream) })
     }
 
     /// `Detector::encode_pertinent_indices` (detector.rs:223-227) for index ciphertext `ct` of the
@@ -450,13 +488,14 @@ impl<'a> Retriever<'a> {
                                  rp.pertinent_count, found_buf.as_mut_ptr(), found_buf.len(), &mut found)
         })?;
         found_buf.truncate(found.min(found_buf.len()));
-        let wrp = RetrievalParams::new(rp.all_payloads_count, found_buf.len())?;
-        let w = payload_weights(seed, &wrp)?;
+        // the board's weights and combination count, whatever the number of indices found
+        // (retriever.rs:196, :215-239)
+        let w = payload_weights(seed, &rp)?;
         let pay = NttRlwe::flatten(payloads_digest);
         let mut out = vec![0u16; found_buf.len() * OMR_PAYLOAD_LEN];
         check(unsafe {
             omr_retrieve_payloads(self.secret.raw, pay.as_ptr(), payloads_digest.len() as u32, rp.all_payloads_count,
-                                  w.as_ptr(), found_buf.as_ptr(), found_buf.len(), out.as_mut_ptr())
+                                  rp.layout.combination_count, w.as_ptr(), found_buf.as_ptr(), found_buf.len(), out.as_mut_ptr())
         })?;
         let payloads = out
             .chunks_exact(OMR_PAYLOAD_LEN)

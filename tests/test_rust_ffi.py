@@ -81,3 +81,31 @@ def test_crate_layout_and_link_directives():
     for api in ("pub fn detect(", "pub fn detect_batch(", "pub fn encode_pertinent_indices(",
                 "pub fn encode_pertinent_payloads(", "pub fn detect_with_time_info(", "pub fn decode_digest("):
         assert api in lib, api
+
+
+def test_detect_time_info_mirrors_reference_struct():
+    """DetectTimeInfo carries the reference struct's fields in its order (detector.rs:51-57:
+    total_detect_time, total_first_level_bootstrapping_time, total_second_level_bootstrapping_time,
+    total_trace_time), as Durations converted from omr_detect_timing."""
+    rs = open(LIB).read()
+    body = re.search(r"pub struct DetectTimeInfo \{(.*?)\n\}", rs, flags=re.S).group(1)
+    assert re.findall(r"pub (\w+): Duration", body) == [
+        "total_detect_time", "total_first_level_bootstrapping_time", "total_second_level_bootstrapping_time",
+        "total_trace_time"]
+    conv = re.search(r"impl From<OmrDetectTiming> for DetectTimeInfo \{(.*?)\n\}", rs, flags=re.S).group(1)
+    for rust_f, c_f in (("total_detect_time", "total_ms"), ("total_first_level_bootstrapping_time", "first_level_ms"),
+                        ("total_second_level_bootstrapping_time", "second_level_ms"), ("total_trace_time", "trace_ms")):
+        assert re.search(rust_f + r": ms\(t\." + c_f + r"\)", conv), rust_f
+    # detect_with_time_info is one locked C call, not an enable / detect / read / disable sequence
+    dwt = re.search(r"pub fn detect_with_time_info\(.*?\n    \}", rs, flags=re.S).group(0)
+    assert "omr_detect_with_time_info(" in dwt and "omr_ctx_enable_timing" not in dwt
+
+
+def test_decode_digest_uses_board_combination_count():
+    """Retriever::decode_digest regenerates the weights with the board's RetrievalParams and solves
+    with its combination count (retriever.rs:196, :215-239), not a count derived from the indices
+    found."""
+    rs = open(LIB).read()
+    dd = re.search(r"pub fn decode_digest\(.*?\n    \}", rs, flags=re.S).group(0)
+    assert "payload_weights(seed, &rp)" in dd and "rp.layout.combination_count" in dd
+    assert "RetrievalParams::new" not in dd

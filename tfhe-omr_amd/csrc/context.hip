@@ -139,13 +139,15 @@ struct omr_ctx {
   // chunks of at most latency_max messages run the latency kernels (latency_kernels.hpp)
   size_t latency_max = OMR_DEFAULT_LATENCY_MAX;
   int *ks_part = nullptr;  // split key-switch partial sums, [KS_SPLIT][64][672][4]
-  // two-CU level-2 latency kernel (br2x_kernel): partial hand-off slots [n][2][2][N2], flags
-  // [n][2], a sticky timeout flag; used when 2 n workgroups fit the CUs at once
+  // two-CU level-2 latency kernel (br2x_kernel, cooperative launch): partial hand-off slots
+  // [n][2][2][N2], flags [n][2], a timeout flag x_err that every launch copies to the pinned host
+  // word x_err_host on its stream (read by omr_ctx_check and at the start of the next call)
   double *x_slots = nullptr;
   uint32_t *x_flags = nullptr;
-  int *x_err = nullptr;
+  int *x_err = nullptr, *x_err_host = nullptr;
   size_t x_cap = 0;
   int num_cu = 0;
+  bool coop = false;  // hipDeviceAttributeCooperativeLaunch
   // host-API staging
   uint16_t *s_clue_a = nullptr, *s_clue_b = nullptr;
   uint64_t *s_out = nullptr;
@@ -162,10 +164,11 @@ struct omr_ctx {
   // summed here so omr_last_timing covers the whole call (device-buffer calls read the events)
   omr_detect_timing host_timing{};
   bool host_timing_valid = false;
-  // timing
-  bool timing = false;
-  std::vector<hipEvent_t> events;  // 4 per chunk
+  // timing: mode 0 off, 1 stage events around the production kernels, 2 trace as its own launch
+  int timing = 0;
+  std::vector<hipEvent_t> events;  // EV_PER_CHUNK per chunk
   size_t timed_messages = 0, timed_chunks = 0;
+  bool timed_split = false;  // the timed call ran the trace as its own launch in every chunk
   std::mutex mu;
 };
 
@@ -303,14 +306,18 @@ omr_status convert_keys_fft1(const uint32_t *host, size_t npoly, double2 *dev, c
 bool latency_path(const omr_ctx *c, size_t n) { return n <= c->latency_max; }
 
 // br2x_kernel's bounded hand-off wait: a workgroup whose partner never published leaves its loop
-// and sets x_err (sticky; reported by the next host-API detect after its stream sync).
-omr_status check_handoff(omr_ctx *c) {
-  if (!c->x_err) return OMR_OK;
-  int e = 0;
-  HIP_TRY(hipMemcpy(&e, c->x_err, sizeof(int), hipMemcpyDeviceToHost));
-  if (!e) return OMR_OK;
+// and sets x_err; each br2x launch then copies x_err to the pinned x_err_host on its stream. This
+// reports (and clears) an error whose copy has landed: callers sync the stream first for a
+// definitive answer (omr_ctx_check, the host entry points), or call it before enqueueing new work
+// (the device entry points) so a failed earlier call is never attributed to a later one.
+omr_status take_handoff_error(omr_ctx *c) {
+  if (!c->x_err_host || !__atomic_load_n(c->x_err_host, __ATOMIC_ACQUIRE)) return OMR_OK;
+  HIP_TRY(hipDeviceSynchronize());  // no launch may still be copying the flag
+  __atomic_store_n(c->x_err_host, 0, __ATOMIC_RELEASE);
   HIP_TRY(hipMemset(c->x_err, 0, sizeof(int)));
-  return set_error(OMR_ERR_DEVICE, "level-2 two-CU hand-off timed out (workgroups not co-resident)");
+  return set_error(OMR_ERR_DEVICE,
+                   "level-2 two-CU hand-off timed out: the output of an earlier detect call on this "
+                   "context is invalid");
 }
 
 // LWE key switch + modulus switch of B messages (lwe1t [1025][B] -> out [B][671]). Up to 64
@@ -342,39 +349,70 @@ omr_status launch_br1(omr_ctx *c, size_t n, const uint16_t *ca, const uint16_t *
   return OMR_OK;
 }
 
-// Level-2 blind rotation (+ trace, mode 0) of n LWE(670, 4096) ciphertexts, one workgroup each.
+// br2x_kernel over 2 n workgroups as a cooperative launch (co-residency guaranteed, or the launch
+// is refused); false when refused, so the caller falls back to br2l_kernel.
+omr_status launch_br2x(omr_ctx *c, size_t n, const uint32_t *lwe_int, uint64_t *out, hipStream_t st,
+                       bool *launched) {
+  *launched = false;
+  if (!c->coop || 2 * n > (size_t)c->num_cu) return OMR_OK;  // one 150 KB-LDS workgroup per CU
+  if (n > c->x_cap) {
+    omr_status s;
+    if ((s = scratch_idle(c)) != OMR_OK) return s;
+    dev_free(c->x_slots);
+    dev_free(c->x_flags);
+    c->x_cap = 0;
+    HIP_TRY(hipMalloc(&c->x_slots, n * 4 * N2 * sizeof(double)));
+    HIP_TRY(hipMalloc(&c->x_flags, n * 2 * sizeof(uint32_t)));
+    c->x_cap = n;
+  }
+  if (!c->x_err) {
+    HIP_TRY(hipMalloc(&c->x_err, sizeof(int)));
+    HIP_TRY(hipMemset(c->x_err, 0, sizeof(int)));
+    HIP_TRY(hipHostMalloc((void **)&c->x_err_host, sizeof(int), hipHostMallocDefault));
+    *c->x_err_host = 0;
+  }
+  HIP_TRY(hipMemsetAsync(c->x_flags, 0, n * 2 * sizeof(uint32_t), st));
+  const double *bsk2 = c->bsk2;
+  DeviceTables tb = c->tb;
+  double *slots = c->x_slots;
+  uint32_t *flags = c->x_flags;
+  int *err = c->x_err;
+  void *args[] = {(void *)&lwe_int, (void *)&bsk2, (void *)&tb, (void *)&slots, (void *)&flags, (void *)&err,
+                  (void *)&out};
+  const hipError_t e = hipLaunchCooperativeKernel(reinterpret_cast<const void *>(&br2x_kernel),
+                                                  dim3((unsigned)(2 * n)), dim3(BR2L_T), args, 0, st);
+  if (e == hipErrorCooperativeLaunchTooLarge || e == hipErrorNotSupported || e == hipErrorInvalidConfiguration) {
+    (void)hipGetLastError();  // refused: nothing was enqueued
+    return OMR_OK;
+  }
+  if (e != hipSuccess) return set_error(OMR_ERR_DEVICE, std::string("br2x cooperative launch: ") + hipGetErrorString(e));
+  HIP_TRY(hipMemcpyAsync(c->x_err_host, c->x_err, sizeof(int), hipMemcpyDeviceToHost, st));
+  *launched = true;
+  return OMR_OK;
+}
+
+// Level-2 blind rotation (+ trace, mode 0) of n LWE(670, 4096) ciphertexts. `mid` (optional) is
+// recorded between the rotation and the trace; with split_trace (timing mode 2) the throughput
+// path runs them as two launches so that the event separates them.
 omr_status launch_br2(omr_ctx *c, size_t n, const uint32_t *lwe_int, uint64_t *out, int mode,
-                      hipStream_t st) {
+                      hipStream_t st, bool split_trace = false, hipEvent_t mid = nullptr) {
   if (latency_path(c, n)) {  // two CUs (or two 4-wave groups) per message, then the trace in place
-    if (2 * n <= (size_t)c->num_cu) {  // every workgroup resident at once (one per CU)
-      if (n > c->x_cap) {
-        omr_status s;
-        if ((s = scratch_idle(c)) != OMR_OK) return s;
-        dev_free(c->x_slots);
-        dev_free(c->x_flags);
-        c->x_cap = 0;
-        HIP_TRY(hipMalloc(&c->x_slots, n * 4 * N2 * sizeof(double)));
-        HIP_TRY(hipMalloc(&c->x_flags, n * 2 * sizeof(uint32_t)));
-        if (!c->x_err) {
-          HIP_TRY(hipMalloc(&c->x_err, sizeof(int)));
-          HIP_TRY(hipMemsetAsync(c->x_err, 0, sizeof(int), st));
-        }
-        c->x_cap = n;
-      }
-      HIP_TRY(hipMemsetAsync(c->x_flags, 0, n * 2 * sizeof(uint32_t), st));
-      br2x_kernel<<<(unsigned)(2 * n), BR2L_T, 0, st>>>(lwe_int, c->bsk2, c->tb, c->x_slots, c->x_flags,
-                                                        c->x_err, out);
-    } else {
-      br2l_kernel<<<(unsigned)n, BR2L_T, 0, st>>>(lwe_int, c->bsk2, c->tb, out);
-    }
-    if (mode == 0) {
-      HIP_TRY(hipGetLastError());
-      trace_kernel<<<(unsigned)n, BR2_T, 0, st>>>(out, c->tk, c->tb);
-    }
+    bool two_cu = false;
+    omr_status s;
+    if ((s = launch_br2x(c, n, lwe_int, out, st, &two_cu)) != OMR_OK) return s;
+    if (!two_cu) br2l_kernel<<<(unsigned)n, BR2L_T, 0, st>>>(lwe_int, c->bsk2, c->tb, out);
+    split_trace = true;
+  } else if (split_trace && mode == 0) {
+    br2_trace_kernel<<<(unsigned)n, BR2_T, 0, st>>>(lwe_int, c->bsk2, c->tk, c->tb, out, 1);
   } else {
     br2_trace_kernel<<<(unsigned)n, BR2_T, 0, st>>>(lwe_int, c->bsk2, c->tk, c->tb, out, mode);
   }
   HIP_TRY(hipGetLastError());
+  if (mid) HIP_TRY(hipEventRecord(mid, st));
+  if (split_trace && mode == 0) {
+    trace_kernel<<<(unsigned)n, BR2_T, 0, st>>>(out, c->tk, c->tb);
+    HIP_TRY(hipGetLastError());
+  }
   return OMR_OK;
 }
 
@@ -400,6 +438,11 @@ extern "C" omr_status omr_ctx_create(const omr_detection_key_view *key, int devi
   auto *c = new omr_ctx();
   c->device = device;
   HIP_TRY(hipDeviceGetAttribute(&c->num_cu, hipDeviceAttributeMultiprocessorCount, device));
+  {
+    int coop = 0;
+    HIP_TRY(hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, device));
+    c->coop = coop != 0;
+  }
   auto fail = [&](omr_status st) {
     omr_ctx_destroy(c);
     return st;
@@ -513,6 +556,7 @@ extern "C" void omr_ctx_destroy(omr_ctx *c) {
   dev_free(c->x_slots);
   dev_free(c->x_flags);
   dev_free(c->x_err);
+  if (c->x_err_host) (void)hipHostFree(c->x_err_host);
   for (auto e : c->events) (void)hipEventDestroy(e);
   if (c->scratch_free) (void)hipEventDestroy(c->scratch_free);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -546,36 +590,55 @@ extern "C" omr_status omr_ctx_set_latency_threshold(omr_ctx *c, size_t max_messa
   return OMR_OK;
 }
 
-extern "C" omr_status omr_ctx_enable_timing(omr_ctx *c, int enable) {
-  if (!c) return set_error(OMR_ERR_INVALID_ARGUMENT, "NULL ctx");
-  c->timing = enable != 0;
+extern "C" omr_status omr_ctx_enable_timing(omr_ctx *c, int mode) {
+  if (!c || mode < 0 || mode > 2) return set_error(OMR_ERR_INVALID_ARGUMENT, "omr_ctx_enable_timing: bad argument");
+  std::lock_guard<std::mutex> lk(c->mu);
+  c->timing = mode;
   return OMR_OK;
+}
+
+extern "C" omr_status omr_ctx_check(omr_ctx *c, void *stream) {
+  if (!c) return set_error(OMR_ERR_INVALID_ARGUMENT, "omr_ctx_check: NULL ctx");
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  if (stream) {
+    HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+  } else {  // the null stream and the context's own (non-blocking) stream
+    HIP_TRY(hipDeviceSynchronize());
+  }
+  return take_handoff_error(c);
 }
 
 namespace {
 
+constexpr int EV_PER_CHUNK = 5;
+
 // Detect D messages of device buffers on st, in chunks of c->batch: per chunk br1f (7 rotations
-// per message) -> sum7 -> key switch -> br2 + trace. Stage events [0] br1 start, [1] br1 end,
-// [2] key switch end, [3] br2 end per chunk.
+// per message) -> sum7 -> key switch -> br2 + trace. Stage events per chunk: [0] br1 start,
+// [1] br1 end, [2] key switch end, [3] level-2 rotation end, [4] trace end ([3] = [4] when the
+// throughput kernel fuses the trace, timing mode 1).
 omr_status detect_device(omr_ctx *c, const uint16_t *ca, const uint16_t *cb, size_t D,
                          uint64_t *out, hipStream_t st) {
   omr_status s;
+  if ((s = take_handoff_error(c)) != OMR_OK) return s;  // an earlier call's output is invalid
   if ((s = ensure_batch(c, std::min(D, c->batch))) != OMR_OK) return s;
   const size_t nchunks = (D + c->batch - 1) / c->batch;
+  const bool split = c->timing == 2;
   if (c->timing) {
-    while (c->events.size() < nchunks * 4) {
+    while (c->events.size() < nchunks * EV_PER_CHUNK) {
       hipEvent_t e;
       HIP_TRY(hipEventCreate(&e));
       c->events.push_back(e);
     }
     c->timed_messages = D;
     c->timed_chunks = nchunks;
+    c->timed_split = true;
   }
   if ((s = scratch_acquire(c, st)) != OMR_OK) return s;
   for (size_t ch = 0; ch < nchunks; ++ch) {
     const size_t off = ch * c->batch;
     const int B = (int)std::min(c->batch, D - off);
-    hipEvent_t *ev = c->timing ? &c->events[ch * 4] : nullptr;
+    hipEvent_t *ev = c->timing ? &c->events[ch * EV_PER_CHUNK] : nullptr;
     if (ev) HIP_TRY(hipEventRecord(ev[0], st));
     if ((s = launch_br1(c, (size_t)B * CLUES, ca + off * N0, cb + off * CLUES, nullptr, nullptr,
                         c->ext, nullptr, 0, st, (size_t)B)) != OMR_OK)
@@ -585,8 +648,10 @@ omr_status detect_device(omr_ctx *c, const uint16_t *ca, const uint16_t *cb, siz
     sum7_kernel<<<(unsigned)((n7 + 255) / 256), 256, 0, st>>>(c->ext, c->lwe1t, B);
     if ((s = launch_ks(c, B, c->lwe_int, st)) != OMR_OK) return s;
     if (ev) HIP_TRY(hipEventRecord(ev[2], st));
-    if ((s = launch_br2(c, (size_t)B, c->lwe_int, out + off * 2 * N2, 0, st)) != OMR_OK) return s;
-    if (ev) HIP_TRY(hipEventRecord(ev[3], st));
+    if ((s = launch_br2(c, (size_t)B, c->lwe_int, out + off * 2 * N2, 0, st, split, ev ? ev[3] : nullptr)) != OMR_OK)
+      return s;
+    if (ev) HIP_TRY(hipEventRecord(ev[4], st));
+    if (ev && !split && !latency_path(c, (size_t)B)) c->timed_split = false;
   }
   return scratch_release(c, st);
 }
@@ -614,24 +679,22 @@ extern "C" omr_status omr_detect_batch_device(omr_ctx *c, const uint16_t *ca, co
   std::lock_guard<std::mutex> lk(c->mu);
   HIP_TRY(hipSetDevice(c->device));
   c->host_timing_valid = false;
-  return detect_device(c, ca, cb, D, out, stream ? (hipStream_t)stream : c->stream);
+  return detect_device(c, ca, cb, D, out, (hipStream_t)stream);  // NULL: HIP's null stream
 }
 
 namespace {
 omr_status collect_timing(omr_ctx *c, omr_detect_timing *t);
 }
 
-extern "C" omr_status omr_detect_batch(omr_ctx *c, const uint16_t *ca, const uint16_t *cb, size_t D,
-                                       uint64_t *out) {
-  if (!c || (D && (!ca || !cb || !out)))
-    return set_error(OMR_ERR_INVALID_ARGUMENT, "omr_detect_batch: NULL argument");
-  if (D == 0) return OMR_OK;
-  std::lock_guard<std::mutex> lk(c->mu);
+namespace {
+// omr_detect_batch with c->mu held.
+omr_status detect_host_locked(omr_ctx *c, const uint16_t *ca, const uint16_t *cb, size_t D, uint64_t *out) {
   HIP_TRY(hipSetDevice(c->device));
   omr_status s;
   const size_t B = std::min(D, c->batch);
   if ((s = stage_buffers(c, B)) != OMR_OK) return s;
   omr_detect_timing acc{};
+  acc.trace_separate = 1;
   c->host_timing_valid = false;
   for (size_t off = 0; off < D; off += B) {
     const size_t n = std::min(B, D - off);
@@ -640,15 +703,17 @@ extern "C" omr_status omr_detect_batch(omr_ctx *c, const uint16_t *ca, const uin
     if ((s = detect_device(c, c->s_clue_a, c->s_clue_b, n, c->s_out, c->stream)) != OMR_OK) return s;
     HIP_TRY(hipMemcpyAsync(out + off * 2 * N2, c->s_out, n * 2 * N2 * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
-    if ((s = check_handoff(c)) != OMR_OK) return s;
+    if ((s = take_handoff_error(c)) != OMR_OK) return s;
     if (c->timing) {
       omr_detect_timing t;
       if ((s = collect_timing(c, &t)) != OMR_OK) return s;
       acc.first_level_ms += t.first_level_ms;
       acc.key_switch_ms += t.key_switch_ms;
       acc.second_level_ms += t.second_level_ms;
+      acc.trace_ms += t.trace_ms;
       acc.total_ms += t.total_ms;
       acc.messages += t.messages;
+      acc.trace_separate &= t.trace_separate;
     }
   }
   if (c->timing) {
@@ -657,36 +722,69 @@ extern "C" omr_status omr_detect_batch(omr_ctx *c, const uint16_t *ca, const uin
   }
   return OMR_OK;
 }
+}  // namespace
+
+extern "C" omr_status omr_detect_batch(omr_ctx *c, const uint16_t *ca, const uint16_t *cb, size_t D,
+                                       uint64_t *out) {
+  if (!c || (D && (!ca || !cb || !out)))
+    return set_error(OMR_ERR_INVALID_ARGUMENT, "omr_detect_batch: NULL argument");
+  if (D == 0) return OMR_OK;
+  std::lock_guard<std::mutex> lk(c->mu);
+  return detect_host_locked(c, ca, cb, D, out);
+}
 
 namespace {
-// Stage times of the last detect_device call from its per-chunk events.
+// Stage times of the last detect_device call from its per-chunk events (DetectTimeInfo's split:
+// first level includes the key switch, detector.rs:183-191).
 omr_status collect_timing(omr_ctx *c, omr_detect_timing *t) {
   memset(t, 0, sizeof(*t));
   if (!c->timing || c->timed_messages == 0) return OMR_OK;
   for (size_t ch = 0; ch < c->timed_chunks; ++ch) {  // the chunk count of the timed call
-    hipEvent_t *ev = &c->events[ch * 4];
-    HIP_TRY(hipEventSynchronize(ev[3]));
-    float a = 0, b = 0, d = 0;
+    hipEvent_t *ev = &c->events[ch * EV_PER_CHUNK];
+    HIP_TRY(hipEventSynchronize(ev[4]));
+    float a = 0, b = 0, d = 0, e = 0;
     HIP_TRY(hipEventElapsedTime(&a, ev[0], ev[1]));
     HIP_TRY(hipEventElapsedTime(&b, ev[1], ev[2]));
     HIP_TRY(hipEventElapsedTime(&d, ev[2], ev[3]));
-    t->first_level_ms += a;
+    HIP_TRY(hipEventElapsedTime(&e, ev[3], ev[4]));
+    t->first_level_ms += a + b;
     t->key_switch_ms += b;
     t->second_level_ms += d;
+    t->trace_ms += e;
   }
-  t->total_ms = t->first_level_ms + t->key_switch_ms + t->second_level_ms;
+  t->total_ms = t->first_level_ms + t->second_level_ms + t->trace_ms;
   t->messages = c->timed_messages;
+  t->trace_separate = c->timed_split ? 1 : 0;
   return OMR_OK;
 }
 }  // namespace
 
 extern "C" omr_status omr_last_timing(omr_ctx *c, omr_detect_timing *t) {
   if (!c || !t) return set_error(OMR_ERR_INVALID_ARGUMENT, "omr_last_timing: NULL argument");
+  std::lock_guard<std::mutex> lk(c->mu);
   if (c->host_timing_valid) {
     *t = c->host_timing;
     return OMR_OK;
   }
+  HIP_TRY(hipSetDevice(c->device));
   return collect_timing(c, t);
+}
+
+extern "C" omr_status omr_detect_with_time_info(omr_ctx *c, const uint16_t *ca, const uint16_t *cb, size_t D,
+                                                uint64_t *out, omr_detect_timing *t) {
+  if (!c || !t || (D && (!ca || !cb || !out)))
+    return set_error(OMR_ERR_INVALID_ARGUMENT, "omr_detect_with_time_info: NULL argument");
+  memset(t, 0, sizeof(*t));
+  t->trace_separate = 1;
+  if (D == 0) return OMR_OK;
+  std::lock_guard<std::mutex> lk(c->mu);
+  const int mode = c->timing;
+  c->timing = 2;
+  omr_status s = detect_host_locked(c, ca, cb, D, out);
+  if (s == OMR_OK) *t = c->host_timing;
+  c->timing = mode;
+  c->host_timing_valid = mode != 0 && s == OMR_OK;
+  return s;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -710,7 +808,7 @@ extern "C" omr_status omr_encode_indices_device(omr_ctx *c, const uint64_t *pv, 
     return set_error(OMR_ERR_INVALID_ARGUMENT, "omr_encode_indices_device: bad argument");
   std::lock_guard<std::mutex> lk(c->mu);
   HIP_TRY(hipSetDevice(c->device));
-  hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+  hipStream_t st = (hipStream_t)stream;  // NULL: HIP's null stream
   omr_retrieval_params rp;
   omr_status s;
   if ((s = omr_get_retrieval_params(all, 0, &rp)) != OMR_OK) return s;
@@ -742,7 +840,7 @@ extern "C" omr_status omr_encode_payloads_device(omr_ctx *c, const uint64_t *pv,
     return set_error(OMR_ERR_INVALID_ARGUMENT, "omr_encode_payloads_device: bad argument");
   std::lock_guard<std::mutex> lk(c->mu);
   HIP_TRY(hipSetDevice(c->device));
-  hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+  hipStream_t st = (hipStream_t)stream;  // NULL: HIP's null stream
   if (D == 0) {
     HIP_TRY(hipMemsetAsync(out, 0, (size_t)n_ct * 2 * N2 * sizeof(uint64_t), st));
     return OMR_OK;
@@ -781,7 +879,7 @@ extern "C" omr_status omr_encode_indices(omr_ctx *c, const uint64_t *pv, size_t 
   HIP_TRY(dpv.alloc(std::max<size_t>(D, 1) * 2 * N2));
   HIP_TRY(dout.alloc(2 * N2));
   HIP_TRY(hipMemcpy(dpv.p, pv, D * 2 * N2 * sizeof(uint64_t), hipMemcpyHostToDevice));
-  omr_status s = omr_encode_indices_device(c, dpv.p, D, offset, all, seed, ct, 1, dout.p, nullptr);
+  omr_status s = omr_encode_indices_device(c, dpv.p, D, offset, all, seed, ct, 1, dout.p, c->stream);
   if (s != OMR_OK) return s;
   HIP_TRY(hipStreamSynchronize(c->stream));
   HIP_TRY(hipMemcpy(out, dout.p, 2 * N2 * sizeof(uint64_t), hipMemcpyDeviceToHost));
@@ -806,7 +904,7 @@ extern "C" omr_status omr_encode_payloads(omr_ctx *c, const uint64_t *pv, const 
   HIP_TRY(hipMemcpy(dpay.p, payloads, D * PAYLOAD_LEN * sizeof(uint16_t), hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(dw.p, weights, wn * sizeof(uint16_t), hipMemcpyHostToDevice));
   omr_status s = omr_encode_payloads_device(c, dpv.p, dpay.p, D, offset, all, dw.p, n_ct, per_ct,
-                                            dout.p, nullptr);
+                                            dout.p, c->stream);
   if (s != OMR_OK) return s;
   HIP_TRY(hipStreamSynchronize(c->stream));
   HIP_TRY(hipMemcpy(out, dout.p, (size_t)n_ct * 2 * N2 * sizeof(uint64_t), hipMemcpyDeviceToHost));
@@ -896,10 +994,13 @@ static omr_status second_level_impl(omr_ctx *c, const uint32_t *lwe, size_t n, u
   HIP_TRY(dl.alloc(n * (NI + 1)));
   HIP_TRY(dout.alloc(n * 2 * N2));
   HIP_TRY(hipMemcpy(dl.p, lwe, n * (NI + 1) * sizeof(uint32_t), hipMemcpyHostToDevice));
-  omr_status ls = launch_br2(c, n, dl.p, dout.p, mode, c->stream);
-  if (ls != OMR_OK) return ls;
-  HIP_TRY(hipGetLastError());
+  omr_status ls;
+  if ((ls = take_handoff_error(c)) != OMR_OK) return ls;
+  if ((ls = scratch_acquire(c, c->stream)) != OMR_OK) return ls;  // the hand-off slots are scratch
+  if ((ls = launch_br2(c, n, dl.p, dout.p, mode, c->stream)) != OMR_OK) return ls;
+  if ((ls = scratch_release(c, c->stream)) != OMR_OK) return ls;
   HIP_TRY(hipStreamSynchronize(c->stream));
+  if ((ls = take_handoff_error(c)) != OMR_OK) return ls;
   HIP_TRY(hipMemcpy(out, dout.p, n * 2 * N2 * sizeof(uint64_t), hipMemcpyDeviceToHost));
   return OMR_OK;
 }

@@ -264,11 +264,14 @@ __global__ __launch_bounds__(BR2L_T, 1) void br2l_kernel(const uint32_t *__restr
 // every storing thread stores its payload with sc1 stores (agent-scope relaxed atomics) and waits
 // vmcnt(0); a workgroup barrier; one lane stores the sc1 flag (step + 1). The consumer's lane 0
 // polls the partner's flag with sc1 loads, a workgroup barrier follows, and every load of the
-// payload is an sc1 load. Payload slots alternate by step parity (the partner cannot publish two
-// steps ahead: each step needs the other's previous partial). The poll is bounded: after
-// BR2X_SPIN polls the workgroup records an error in *err and leaves the loop, so every wave
-// exits. The grid (2 workgroups per message, one per CU) must be co-resident: the launch checks
-// it against the CU count.
+// payload is an sc1 load. Steps with a_i = 0 are skipped by both workgroups, so the hand-offs are
+// numbered by a counter h of EXECUTED steps: the flag carries h + 1 and the payload slot is h & 1.
+// Consecutive hand-offs therefore alternate slots, and before a workgroup rewrites slot h & 1 (at
+// hand-off h + 2) it has seen the partner's flag h + 2, which the partner publishes only after
+// its hand-off-h read of that slot was consumed. The poll is bounded: after BR2X_SPIN polls the
+// workgroup records an error in *err and leaves the loop, so every wave exits. The grid (2
+// workgroups per message, one per CU) must be co-resident: the host launches it with
+// hipLaunchCooperativeKernel, which guarantees that or refuses the launch.
 constexpr int BR2X_SPIN = 1 << 24;
 
 __device__ __forceinline__ void st_sc1(double *p, double v) {
@@ -317,10 +320,12 @@ __global__ __launch_bounds__(BR2L_T, 1) void br2x_kernel(const uint32_t *__restr
     __syncthreads();
   }
   uint32_t *my_flag = flags + 2 * m + r, *their_flag = flags + 2 * m + (1 - r);
+  uint32_t h = 0;  // hand-offs so far (executed steps)
 #pragma unroll 1
   for (int i = 0; i < NI; ++i) {
     const int a = (int)__builtin_amdgcn_readfirstlane(lwe[i]) & (2 * N - 1);
     if (a == 0) continue;  // (X^0 - 1) * ACC = 0 (both workgroups of the message skip it)
+    const size_t slot = h & 1;
     const double *ggsw = bsk2 + ((size_t)i * 2 * D2 + (size_t)r * D2 + (size_t)g * KD) * 2 * N;
     uint32_t pk[E][DG::DW];
     {  // digits of (X^a - 1) * ACC_r: group 0 stages ACC_r, both groups decompose it
@@ -374,15 +379,15 @@ __global__ __launch_bounds__(BR2L_T, 1) void br2x_kernel(const uint32_t *__restr
         const double sa = red<M>(red<M>(accA[e]) + part[0][t * E + e]);
         const double sb = red<M>(red<M>(accB[e]) + part[1][t * E + e]);
         keep[e] = r == 0 ? sa : sb;
-        st_sc1(xg + (((size_t)m * 2 + r) * 2 + (i & 1)) * N + t * E + e, r == 0 ? sb : sa);  // the partner's output
+        st_sc1(xg + (((size_t)m * 2 + r) * 2 + slot) * N + t * E + e, r == 0 ? sb : sa);  // the partner's output
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-      __hip_atomic_store(my_flag, (uint32_t)(i + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(my_flag, h + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       int n = 0;
-      while (__hip_atomic_load(their_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (uint32_t)(i + 1)) {
+      while (__hip_atomic_load(their_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < h + 1) {
         if (++n == BR2X_SPIN) {
           stop = 1;
           atomicExch(err, 1);
@@ -397,13 +402,14 @@ __global__ __launch_bounds__(BR2L_T, 1) void br2x_kernel(const uint32_t *__restr
       double s[E];
 #pragma unroll
       for (int e = 0; e < E; ++e)
-        s[e] = red<M>(keep[e] + ld_sc1(xg + (((size_t)m * 2 + (1 - r)) * 2 + (i & 1)) * N + t * E + e));
+        s[e] = red<M>(keep[e] + ld_sc1(xg + (((size_t)m * 2 + (1 - r)) * 2 + slot) * N + t * E + e));
       NTT::template inv<0>(s, X, tw, t, tb.tw2c);
 #pragma unroll
       for (int e = 0; e < E; ++e) acc[e] = canon<M>(acc[e] + s[e]);
     } else {
       __syncthreads();  // the inverse's one workgroup barrier (its cross-wave exchange)
     }
+    ++h;
   }
   if (g == 0) {
     uint64_t *o = out + (size_t)m * 2 * N + (size_t)r * N;

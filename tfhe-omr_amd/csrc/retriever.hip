@@ -75,14 +75,16 @@ extern "C" omr_status omr_retrieve_indices(const omr_secret_key_pack *sk, const 
 
 extern "C" omr_status omr_retrieve_payloads(const omr_secret_key_pack *sk, const uint64_t *pay_cts,
                                             uint32_t n_ct, size_t all_payloads_count,
-                                            const uint16_t *weights, const size_t *indices,
+                                            uint32_t combination_count, const uint16_t *weights,
+                                            const size_t *indices,
                                             size_t n_indices, uint16_t *payloads) {
   if (!sk || !pay_cts || !weights || (n_indices && (!indices || !payloads)))
     return set_error(OMR_ERR_INVALID_ARGUMENT, "omr_retrieve_payloads: NULL argument");
   omr_retrieval_params rp;
   omr_status st = omr_get_retrieval_params(all_payloads_count, n_indices, &rp);
   if (st != OMR_OK) return st;
-  const size_t rows = rp.combination_count, cols = n_indices, per = rp.cmb_count_per_cipher;
+  const size_t rows = combination_count ? combination_count : rp.combination_count, cols = n_indices,
+               per = rp.cmb_count_per_cipher;
   if (n_indices == 0) return OMR_OK;
   if ((size_t)n_ct * per < rows)
     return set_error(OMR_ERR_INVALID_ARGUMENT, "omr_retrieve_payloads: too few payload ciphertexts");

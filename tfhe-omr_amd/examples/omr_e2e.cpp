@@ -140,7 +140,7 @@ int main(int argc, char **argv) {
   CHECK(omr_retrieve_indices(pa, idx_ct.data(), n_idx, D, pert_count, found.data(), found.size(), &nfound));
   found.resize(std::min(nfound, found.size()));
   std::vector<uint16_t> solved(found.size() * PAYLOAD);
-  CHECK(omr_retrieve_payloads(pa, pay_ct.data(), n_pay, D, weights.data(), found.data(), found.size(),
+  CHECK(omr_retrieve_payloads(pa, pay_ct.data(), n_pay, D, rp.combination_count, weights.data(), found.data(), found.size(),
                               solved.data()));
   std::printf("decode time: %.3f s\n", secs(t));
 

@@ -46,8 +46,10 @@ class _KeyView(C.Structure):
 
 
 class _Timing(C.Structure):
-    _fields_ = [("total_ms", C.c_float), ("first_level_ms", C.c_float), ("key_switch_ms", C.c_float),
-                ("second_level_ms", C.c_float), ("messages", C.c_size_t)]
+    """omr_detect_timing: DetectTimeInfo (detector.rs:51-57) in milliseconds of device time."""
+    _fields_ = [("total_ms", C.c_float), ("first_level_ms", C.c_float), ("second_level_ms", C.c_float),
+                ("trace_ms", C.c_float), ("key_switch_ms", C.c_float), ("messages", C.c_size_t),
+                ("trace_separate", C.c_int)]
 
 
 EXPORTS = {
@@ -74,6 +76,8 @@ EXPORTS = {
     "omr_detect_batch_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p]),
     "omr_ctx_enable_timing": (C.c_int, [C.c_void_p, C.c_int]),
     "omr_last_timing": (C.c_int, [C.c_void_p, C.POINTER(_Timing)]),
+    "omr_detect_with_time_info": (C.c_int, [C.c_void_p, _u16p, _u16p, C.c_size_t, _u64p, C.POINTER(_Timing)]),
+    "omr_ctx_check": (C.c_int, [C.c_void_p, C.c_void_p]),
     "omr_encode_indices": (C.c_int, [C.c_void_p, _u64p, C.c_size_t, C.c_size_t, C.c_size_t, C.c_uint64,
                                      C.c_uint32, _u64p]),
     "omr_encode_indices_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_size_t, C.c_size_t,
@@ -90,7 +94,7 @@ EXPORTS = {
     "omr_retrieve_indices": (C.c_int, [C.c_void_p, _u64p, C.c_uint32, C.c_size_t, C.c_size_t,
                                        np.ctypeslib.ndpointer(dtype=np.uintp, flags="C_CONTIGUOUS"),
                                        C.c_size_t, C.POINTER(C.c_size_t)]),
-    "omr_retrieve_payloads": (C.c_int, [C.c_void_p, _u64p, C.c_uint32, C.c_size_t, _u16p,
+    "omr_retrieve_payloads": (C.c_int, [C.c_void_p, _u64p, C.c_uint32, C.c_size_t, C.c_uint32, _u16p,
                                         np.ctypeslib.ndpointer(dtype=np.uintp, flags="C_CONTIGUOUS"),
                                         C.c_size_t, _u16p]),
     "omr_second_level": (C.c_int, [C.c_void_p, _u32p, C.c_size_t, _u64p]),
@@ -331,14 +335,16 @@ class Retriever:
         idx = np.ascontiguousarray(sorted(indices), dtype=np.uintp)
         out = np.zeros((len(idx), PAYLOAD_LENGTH), np.uint16)
         _check(lib().omr_retrieve_payloads(self._sk._h, cts.reshape(-1), cts.shape[0], rp.all_payloads_count,
+                                           rp.combination_count,
                                            np.ascontiguousarray(weights, dtype=np.uint16).reshape(-1), idx,
                                            len(idx), out.reshape(-1)), "omr_retrieve_payloads")
         return out
 
     def decode_digest(self, idx_cts, pay_cts, seed: bytes):
-        """Retriever::decode_digest: sorted pertinent indices and their payloads (mod 257)."""
+        """Retriever::decode_digest: sorted pertinent indices and their payloads (mod 257); the
+        weights and the system's rows follow the board's RetrievalParams (retriever.rs:196, :215-239)."""
         indices = self.decode_pertinent_indices(idx_cts)
-        weights = payload_weights(seed, RetrievalParams(self.params.all_payloads_count, len(indices)))
+        weights = payload_weights(seed, self.params)
         return indices, self.decode_combined_payloads_and_solve(pay_cts, weights, indices)
 
 
@@ -411,21 +417,34 @@ class Detector:
         _check(lib().omr_detect_batch_device(self._h, d_clue_a, d_clue_b, D, d_out, stream or None),
                "omr_detect_batch_device")
 
-    def enable_timing(self, on: bool = True):
-        _check(lib().omr_ctx_enable_timing(self._h, int(on)), "omr_ctx_enable_timing")
+    def check(self, stream: int = 0):
+        """omr_ctx_check: sync `stream` (0: the whole device) and raise if an earlier call's device
+        work failed."""
+        _check(lib().omr_ctx_check(self._h, stream or None), "omr_ctx_check")
+
+    def enable_timing(self, mode: int = 1):
+        """0 off; 1 stage events around the production kernels (the throughput path fuses the
+        trace into level 2); 2 the reference's split (trace as its own launch)."""
+        _check(lib().omr_ctx_enable_timing(self._h, int(mode)), "omr_ctx_enable_timing")
 
     def last_timing(self) -> dict:
         t = _Timing()
         _check(lib().omr_last_timing(self._h, C.byref(t)), "omr_last_timing")
         return {n: getattr(t, n) for n, _ in _Timing._fields_}
 
-    # detect_with_time_info (detector.rs:169-221): stage split of one batch (device time)
+    # detect_with_time_info (detector.rs:169-221): DetectTimeInfo of one batch (device time),
+    # detect + timing in one locked call
     def detect_with_time_info(self, clue_a, clue_b):
-        self.enable_timing(True)
-        out = self.detect_batch(clue_a, clue_b)
-        info = self.last_timing()
-        self.enable_timing(False)
-        return out, info
+        clue_a = np.ascontiguousarray(clue_a, dtype=np.uint16)
+        clue_b = np.ascontiguousarray(clue_b, dtype=np.uint16)
+        D = clue_a.shape[0]
+        if clue_a.shape != (D, N0) or clue_b.shape != (D, CLUE_COUNT):
+            raise OmrError("clues must be u16 [D][512] and [D][7]")
+        out = np.empty((D, 2, N2), np.uint64)
+        t = _Timing()
+        _check(lib().omr_detect_with_time_info(self._h, clue_a.reshape(-1), clue_b.reshape(-1), D, out.reshape(-1),
+                                               C.byref(t)), "omr_detect_with_time_info")
+        return out, {n: getattr(t, n) for n, _ in _Timing._fields_}
 
     # encode_pertinent_indices (detector.rs:223-339)
     def encode_pertinent_indices(self, rp: RetrievalParams, pertinency_vector, seed: int, ct: int = 0,

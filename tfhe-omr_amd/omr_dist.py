@@ -50,12 +50,21 @@ class Digest:
     payloads: np.ndarray  # u64 [n_pay_ct][2][2048]
 
 
+def _on_backend(t, dist):
+    """`t` where the process group's backend can reduce it: host memory for gloo."""
+    if t.is_cuda and dist.get_backend() == "gloo":
+        return t.cpu()
+    return t
+
+
 def reduce_digest(local, dist=None, dst: int = 0):
     """Sum the partial digests (torch.int64 [n_ct][2][2048], canonical < q2 < 2^50; the int64
     sum is exact up to 8,192 ranks) over the ranks with one reduce, and reduce mod q2 on `dst`.
-    Returns the digest (numpy u64) on dst, None elsewhere. `local` lives where the process
-    group's backend wants it (device memory for RCCL, host memory for gloo)."""
+    Returns the digest (numpy u64) on dst, None elsewhere. RCCL reduces `local` where it is
+    (device memory); a gloo group gets device partials staged to host memory first (gloo has no
+    device tensors), so the GPU backend also runs under gloo (tests/test_dist_gpu.py)."""
     if dist is not None and dist.is_initialized() and dist.get_world_size() > 1:
+        local = _on_backend(local, dist)
         dist.reduce(local, dst=dst, op=dist.ReduceOp.SUM)
         if dist.get_rank() != dst:
             return None
@@ -80,7 +89,7 @@ def encode_and_reduce(backend, pv, payloads, first: int, total: int, rp, index_s
     t2 = time.perf_counter()
     times = [t1 - t0, t2 - t0]
     if dist is not None and dist.is_initialized() and dist.get_world_size() > 1:
-        tt = torch.tensor(times, dtype=torch.float64, device=local.device)
+        tt = _on_backend(torch.tensor(times, dtype=torch.float64, device=local.device), dist)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         times = tt.tolist()
     timing = {"encode_s": times[0], "encode_reduce_s": times[1]}
@@ -110,8 +119,8 @@ class GpuBackend:
         self._weights = None
 
     def synchronize(self):
-        import torch
-        torch.cuda.synchronize(self.device)
+        """Wait for the stream and surface any device-side failure of the detect calls."""
+        self.det.check(self.stream.cuda_stream)
 
     def detect(self, clue_a, clue_b, out=None):
         """clue_a int16 [D][512], clue_b int16 [D][7] device tensors -> pv int64 [D][2][2048]."""
