@@ -77,17 +77,29 @@ __global__ __launch_bounds__(64 * BR1L_WAVES, 1) void br1l_kernel(
   for (int j = threadIdx.x; j < NF; j += 64 * W) tws[j] = tb.fft1[j];
   for (int j = threadIdx.x; j < 2 * 2 * 8 * 64; j += 64 * W) (&sum[0][0][0])[j] = 0.0;
   __syncthreads();
-#pragma unroll 1
-  for (int i = 0; i < N0; ++i) {
-    const int a = __builtin_amdgcn_readfirstlane(la[i]);
-    if (a == 0) continue;  // (X^0 - 1) * ACC = 0 (a is uniform over the workgroup)
+  // GGSW row `wave` of the next executed step is loaded one step ahead (issued after this step's
+  // multiply-accumulate, in flight across the inverse and the next digits + transform): a lone
+  // message's rows come from HBM / the Infinity Cache, and a step takes ~7 us.
+  auto next_step = [&](int i) {  // first i' >= i with a_i' != 0 (uniform)
+    while (i < N0 && la[i] == 0) ++i;
+    return i;
+  };
+  double2 kk[2][8];  // [output A/B][point]
+  auto load_row = [&](int i) {
+    if (i >= N0) return;
     const double2 *kr = bskf + ((size_t)i * 2 * D1 + wave) * 2 * NF + lane * 8;  // GGSW row `wave`
-    double2 kk[2][8];  // [output A/B][point]
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       kk[0][e] = kr[e];
       kk[1][e] = kr[NF + e];
     }
+  };
+  int i = next_step(0), inext;
+  load_row(i);
+#pragma unroll 1
+  for (; i < N0; i = inext) {
+    const int a = __builtin_amdgcn_readfirstlane(la[i]);  // != 0: (X^0 - 1) * ACC = 0 is skipped
+    inext = __builtin_amdgcn_readfirstlane(next_step(i + 1));
     double xr[1][8], xi[1][8];
     const int base = lane - a + 2 * N1;
 #pragma unroll
@@ -110,6 +122,7 @@ __global__ __launch_bounds__(64 * BR1L_WAVES, 1) void br1l_kernel(
         __hip_atomic_fetch_add(&sum[t][0][e * 64 + lane], re, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         __hip_atomic_fetch_add(&sum[t][1][e * 64 + lane], im, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
+    load_row(inext);
     __syncthreads();
     if (wave < 2) {  // wave 0: output A (mask accumulator), wave 1: output B (body accumulator)
       double sr[1][8], si[1][8];
@@ -265,12 +278,12 @@ __global__ __launch_bounds__(BR2L_T, 1) void br2l_kernel(const uint32_t *__restr
 // vmcnt(0); a workgroup barrier; one lane stores the sc1 flag (step + 1). The consumer's lane 0
 // polls the partner's flag with sc1 loads, a workgroup barrier follows, and every load of the
 // payload is an sc1 load. Steps with a_i = 0 are skipped by both workgroups, so the hand-offs are
-// numbered by a counter h of EXECUTED steps: the flag carries h + 1 and the payload slot is h & 1.
-// Consecutive hand-offs therefore alternate slots, and before a workgroup rewrites slot h & 1 (at
-// hand-off h + 2) it has seen the partner's flag h + 2, which the partner publishes only after
-// its hand-off-h read of that slot was consumed. The poll is bounded: after BR2X_SPIN polls the
-// workgroup records an error in *err and leaves the loop, so every wave exits. The grid (2
-// workgroups per message, one per CU) must be co-resident: the host launches it with
+// numbered by a counter hc of EXECUTED steps: the flag carries hc + 1 and the payload slot is
+// hc & 1. Consecutive hand-offs therefore alternate slots, and before a workgroup rewrites slot
+// hc & 1 (at hand-off hc + 2) it has seen the partner's flag hc + 2, which the partner publishes
+// only after its hand-off-hc read of that slot was consumed. The poll is bounded: after BR2X_SPIN
+// polls the workgroup records an error in *err and leaves the loop, so every wave exits. The grid
+// (2 workgroups per message, one per CU) must be co-resident: the host launches it with
 // hipLaunchCooperativeKernel, which guarantees that or refuses the launch.
 constexpr int BR2X_SPIN = 1 << 24;
 
@@ -320,12 +333,12 @@ __global__ __launch_bounds__(BR2L_T, 1) void br2x_kernel(const uint32_t *__restr
     __syncthreads();
   }
   uint32_t *my_flag = flags + 2 * m + r, *their_flag = flags + 2 * m + (1 - r);
-  uint32_t h = 0;  // hand-offs so far (executed steps)
+  uint32_t hc = 0;  // hand-offs so far (executed steps)
 #pragma unroll 1
   for (int i = 0; i < NI; ++i) {
     const int a = (int)__builtin_amdgcn_readfirstlane(lwe[i]) & (2 * N - 1);
     if (a == 0) continue;  // (X^0 - 1) * ACC = 0 (both workgroups of the message skip it)
-    const size_t slot = h & 1;
+    const size_t slot = hc & 1;
     const double *ggsw = bsk2 + ((size_t)i * 2 * D2 + (size_t)r * D2 + (size_t)g * KD) * 2 * N;
     uint32_t pk[E][DG::DW];
     {  // digits of (X^a - 1) * ACC_r: group 0 stages ACC_r, both groups decompose it
@@ -385,9 +398,9 @@ __global__ __launch_bounds__(BR2L_T, 1) void br2x_kernel(const uint32_t *__restr
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-      __hip_atomic_store(my_flag, h + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(my_flag, hc + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       int n = 0;
-      while (__hip_atomic_load(their_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < h + 1) {
+      while (__hip_atomic_load(their_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < hc + 1) {
         if (++n == BR2X_SPIN) {
           stop = 1;
           atomicExch(err, 1);
@@ -409,7 +422,7 @@ __global__ __launch_bounds__(BR2L_T, 1) void br2x_kernel(const uint32_t *__restr
     } else {
       __syncthreads();  // the inverse's one workgroup barrier (its cross-wave exchange)
     }
-    ++h;
+    ++hc;
   }
   if (g == 0) {
     uint64_t *o = out + (size_t)m * 2 * N + (size_t)r * N;
