@@ -1,0 +1,75 @@
+"""The level-2 exact-FFT kernel's transform (tfhe-omr_amd/csrc/br2_fft.hpp, Fft1024) restated in
+numpy (tests/fft2_model.py): layouts, permlane relayouts, LDS exchanges and twiddle tree must give
+the exact negacyclic product after rounding, with margin, for the external product's worst case
+(12 GGSW rows of 2048 digits |d| <= 64 against 25-bit key limbs |k| <= 2^24); every LDS exchange
+and the rotation staging must be bank-conflict free under the MI355X lane-group rules."""
+import numpy as np
+import pytest
+
+import fft2_model as M
+
+
+def test_layouts_are_bijections_and_relayouts_match():
+    for p in M.IDX:
+        assert sorted(M.IDX[p].ravel().tolist()) == list(range(M.n))
+    assert np.array_equal(M.relayout_perm(M.IDX[0].copy()), M.IDX[1])
+    assert np.array_equal(M.relayout_perm(M.IDX[2].copy()), M.IDX[3])
+    # exchanges: X moves the wave bits, W keeps each wave's points inside the wave
+    assert not np.array_equal(M.IDX[1] >> 4 & 3, M.IDX[2] >> 4 & 3)
+    for t in range(M.T):
+        assert {M.idx(3, t, e) >> 6 & 3 for e in range(M.E)} == {M.idx(4, t, e) >> 6 & 3 for e in range(M.E)}
+
+
+@pytest.mark.parametrize("name", sorted(M.SWIZZLES))
+def test_exchanges_conflict_free(name):
+    sw = M.SWIZZLES[name]
+    assert sorted(sw(j) for j in range(M.n)) == list(range(M.n))
+    assert M.exchange_cycles(name) == (8.0, 4.0)
+
+
+def test_rotation_staging_conflict_free():
+    w = r = 0
+    for wave in range(4):
+        for e in range(M.E):
+            for h in (0, M.n):
+                cs = [M.idx(0, wave * 64 + l, e) + h for l in range(64)]
+                w = max(w, M.lds_cycles([M.slot_stage(c) * 8 for c in cs], M.WRITE_B64, 32, 8))
+                for a in (1, 63, 64, 65, 1000, 2047, 2048, 4095):
+                    rs = [((c - a) % 4096) % 2048 for c in cs]
+                    r = max(r, M.lds_cycles([M.slot_stage(x) * 8 for x in rs], M.READ_B64, 64, 8))
+    assert (w, r) == (4, 2)
+
+
+def test_twiddle_table_layout():
+    tab = M.twiddle_table()
+    assert len(tab) == 1020 and np.allclose(np.abs(tab), 1.0)
+    # pass-0 constants of the device code: B = e^{i pi/8}, A = e^{i pi/4}, AB = e^{3 i pi/8}
+    B, A, AB = M.block_tw(0, 0)
+    assert np.allclose([B, A, AB], np.exp(1j * np.pi * np.array([1, 2, 3]) / 8))
+
+
+def _exact(d, k):
+    return sum(np.array(M.negacyclic(d[r], k[r]), dtype=object) for r in range(len(d)))
+
+
+def test_product_exact_random_and_adversarial():
+    rng = np.random.default_rng(7)
+    N = 2 * M.n
+    d = rng.integers(-64, 65, (12, N))
+    k = rng.integers(-2**24, 2**24 + 1, (12, N))
+    got = M.product(d, k)
+    want = _exact(d, k)
+    assert np.array_equal(np.rint(got).astype(np.int64).astype(object), want)
+    assert np.max(np.abs(got - want.astype(np.float64))) < 0.05
+    # adversarial: every term of output coefficient c at its maximum with one sign (|coef| ~ 2^44.6)
+    for c in (0, 1023, 2047):
+        kk = rng.choice([-2**24, 2**24], (12, N))
+        j = np.arange(N)
+        src = (c - j) % N
+        sign = np.where(j <= c, 1, -1)
+        dd = 64 * sign[None, :] * np.sign(kk[:, src])
+        got = M.product(dd, kk)
+        want = _exact(dd, kk)
+        err = np.max(np.abs(got - want.astype(np.float64)))
+        assert abs(float(want[c])) > 2**44 and err < 0.1, (c, err)
+        assert np.array_equal(np.rint(got).astype(np.int64).astype(object), want)

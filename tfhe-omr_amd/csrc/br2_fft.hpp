@@ -1,0 +1,460 @@
+// Level-2 blind rotation on the exact complex FFT (second_level_bootstrapping, detector.rs:599-624).
+//
+// The external product only multiplies gadget digits (|d| <= 64) by key residues, so with the
+// key split into two 25-bit limbs, k = k_lo + 2^25 k_hi (|k_lo|, |k_hi| <= 2^24), every coefficient
+// of sum_r d_r * k_r,limb over the 12 GGSW rows is an integer below 12 * 2048 * 64 * 2^24 < 2^44.6,
+// and an FP64 FFT product rounds to it exactly (tests/fft2_model.py: worst error ~1e-2 with
+// adversarial digits; tests/test_fft2_layout.py). The limb products are recombined mod q2 as
+// red(P_hi * 2^25) + P_lo (2^25 P_hi is an exact double). Same digits and rows as the NTT kernels,
+// so the output is bit-identical to them.
+//
+// Transform (Fft1024): R[X]/(X^2048 + 1) -> C[X]/(X^1024 - i), z_j = p_j + i p_{j+1024}; 1,024
+// complex points on 256 threads x 4 registers, five radix-4 passes of the twiddle tree of
+// device_fft.hpp (n = 1024). Index bits j9..j0, pass P holds bits (9 - 2P, 8 - 2P) in registers
+// e = (e1, e0); layouts (position bits e1 e0 | lane l5..l0 | wave w1 w0 -> index bits):
+//   P0: 9 8 | 7 6 3 2 1 0 | 5 4    (input: coefficient pairs (j, j + 1024) of point j)
+//   P1: 7 6 | 9 8 3 2 1 0 | 5 4    P0 -> P1: register bits 1, 0 <-> lane bits 5, 4 (permlane swaps)
+//   P2: 5 4 | 3 2 1 0 9 8 | 7 6    P1 -> P2: cross-wave LDS exchange (X0 / X1)
+//   P3: 3 2 | 5 4 1 0 9 8 | 7 6    P2 -> P3: permlane swaps
+//   P4: 1 0 | 5 4 3 2 9 8 | 7 6    P3 -> P4: wave-local LDS exchange (W); the multiply-accumulate
+//                                  layout: thread t holds points 4t..4t+3 of the key's storage order
+// Each exchange has its own XOR swizzle, conflict-free for the ds_write_b128 8-lane and
+// ds_read_b128 16-lane groups in its direction (tests/test_fft2_layout.py models the banks).
+// Per CMUX step: 12 forward transforms, 48 complex multiply-accumulates per point, 4 inverse
+// transforms (2 outputs x 2 limbs) instead of the NTT kernel's 12 + 2 modular transforms.
+#pragma once
+
+#include "latency_kernels.hpp"
+
+namespace omr {
+
+struct Fft1024 {
+  static constexpr int T = 256, E = 4, n = 1024, L = 10;
+  static constexpr int TW_LEN = 3 * (4 + 16 + 64 + 256);  // passes 1..4: (B, A, AB) per block
+  __device__ static constexpr int tw_off(int p) { return p == 1 ? 0 : p == 2 ? 12 : p == 3 ? 60 : 252; }
+
+  // index bit of each position bit (e1, e0, l5, l4, l3, l2, l1, l0, w1, w0), per pass layout
+  OMR_HD static constexpr int lay(int p, int k) {
+    constexpr int tab[5][10] = {{9, 8, 7, 6, 3, 2, 1, 0, 5, 4},
+                                {7, 6, 9, 8, 3, 2, 1, 0, 5, 4},
+                                {5, 4, 3, 2, 1, 0, 9, 8, 7, 6},
+                                {3, 2, 5, 4, 1, 0, 9, 8, 7, 6},
+                                {1, 0, 5, 4, 3, 2, 9, 8, 7, 6}};
+    return tab[p][k];
+  }
+  // point index held by register e of thread t in pass layout p
+  OMR_HD static constexpr int idx(int p, int t, int e) {
+    const int pos[10] = {(e >> 1) & 1, e & 1, (t >> 5) & 1, (t >> 4) & 1, (t >> 3) & 1, (t >> 2) & 1,
+                         (t >> 1) & 1, t & 1, (t >> 7) & 1, (t >> 6) & 1};
+    int j = 0;
+    for (int k = 0; k < 10; ++k) j |= pos[k] << lay(p, k);
+    return j;
+  }
+  OMR_HD static constexpr int bit(int j, int b) { return (j >> b) & 1; }
+  // exchange swizzles: slot bits s0..s9 as XORs of index bits (tests/fft2_model.py SWIZZLES)
+  OMR_HD static constexpr int slot_xf(int j) {  // P1 -> P2
+    return bit(j, 0) | bit(j, 1) << 1 | (bit(j, 2) ^ bit(j, 8)) << 2 | bit(j, 9) << 3 | bit(j, 8) << 4 |
+           bit(j, 3) << 5 | ((j >> 4) & 15) << 6;
+  }
+  OMR_HD static constexpr int slot_xi(int j) {  // P2 -> P1
+    return bit(j, 0) | (bit(j, 1) ^ bit(j, 8)) << 1 | (bit(j, 2) ^ bit(j, 9)) << 2 | bit(j, 3) << 3 |
+           bit(j, 8) << 4 | bit(j, 9) << 5 | ((j >> 4) & 15) << 6;
+  }
+  OMR_HD static constexpr int slot_wf(int j) {  // P3 -> P4 (wave bits j7 j6 -> slot bits 9 8)
+    return bit(j, 8) | bit(j, 9) << 1 | (bit(j, 2) ^ bit(j, 0)) << 2 | bit(j, 3) << 3 | bit(j, 0) << 4 |
+           bit(j, 1) << 5 | ((j >> 4) & 15) << 6;
+  }
+  OMR_HD static constexpr int slot_wi(int j) {  // P4 -> P3
+    return bit(j, 8) | bit(j, 9) << 1 | (bit(j, 2) ^ bit(j, 0)) << 2 | bit(j, 1) << 3 | bit(j, 0) << 4 |
+           bit(j, 3) << 5 | ((j >> 4) & 15) << 6;
+  }
+  // rotation staging of 2048 real coefficients (doubles): conflict-free ds_write_b64 / ds_read_b64
+  OMR_HD static constexpr int slot_stage(int c) { return c ^ (((c >> 6) & 1) << 4); }
+
+  // pass-0 twiddles (block 0): B = w^256 = e^{i pi / 8}, A = w^512 = e^{i pi / 4}, AB = e^{3 i pi / 8}
+  static constexpr double C8 = 0.92387953251128675613, S8 = 0.38268343236508977173, R2 = 0.70710678118654752440;
+
+  __device__ static __forceinline__ void cmul(double &xr, double &xi, double wr, double wi) {
+    const double r = __fma_rn(xr, wr, -xi * wi);
+    const double i = __fma_rn(xr, wi, xi * wr);
+    xr = r;
+    xi = i;
+  }
+  __device__ static __forceinline__ void cmulc(double &xr, double &xi, double wr, double wi) {  // * conj(w)
+    const double r = __fma_rn(xr, wr, xi * wi);
+    const double i = __fma_rn(xi, wr, -xr * wi);
+    xr = r;
+    xi = i;
+  }
+  // radix-4 network after y = T * x: (a0 + a1, a0 - a1, b0 + i b1, b0 - i b1)
+  __device__ static __forceinline__ void net4(double (&xr)[E], double (&xi)[E]) {
+    const double a0r = xr[0] + xr[2], a0i = xi[0] + xi[2], b0r = xr[0] - xr[2], b0i = xi[0] - xi[2];
+    const double a1r = xr[1] + xr[3], a1i = xi[1] + xi[3], b1r = xr[1] - xr[3], b1i = xi[1] - xi[3];
+    xr[0] = a0r + a1r;
+    xi[0] = a0i + a1i;
+    xr[1] = a0r - a1r;
+    xi[1] = a0i - a1i;
+    xr[2] = b0r - b1i;
+    xi[2] = b0i + b1r;
+    xr[3] = b0r + b1i;
+    xi[3] = b0i - b1r;
+  }
+  // adjoint network (4 x its inverse): y0 = a0 + b0, y1 = a1 + b1, y2 = a0 - b0, y3 = a1 - b1
+  __device__ static __forceinline__ void inet4(double (&xr)[E], double (&xi)[E]) {
+    const double a0r = xr[0] + xr[1], a0i = xi[0] + xi[1], a1r = xr[0] - xr[1], a1i = xi[0] - xi[1];
+    const double b0r = xr[2] + xr[3], b0i = xi[2] + xi[3];
+    const double b1r = xi[2] - xi[3], b1i = xr[3] - xr[2];  // -i (o2 - o3)
+    xr[0] = a0r + b0r;
+    xi[0] = a0i + b0i;
+    xr[2] = a0r - b0r;
+    xi[2] = a0i - b0i;
+    xr[1] = a1r + b1r;
+    xi[1] = a1i + b1i;
+    xr[3] = a1r - b1r;
+    xi[3] = a1i - b1i;
+  }
+  template <int P>
+  __device__ static __forceinline__ int block(int t) {
+    return idx(P, t, 0) >> (L - 2 * P);
+  }
+  template <int P>
+  __device__ static __forceinline__ void fwd_pass(double (&xr)[E], double (&xi)[E], const double2 *tws, int t) {
+    if constexpr (P == 0) {
+      cmul(xr[1], xi[1], C8, S8);
+      cmul(xr[2], xi[2], R2, R2);
+      cmul(xr[3], xi[3], S8, C8);
+    } else {
+      const double2 *w = tws + tw_off(P) + 3 * block<P>(t);
+      const double2 B = w[0], A = w[1], AB = w[2];
+      cmul(xr[1], xi[1], B.x, B.y);
+      cmul(xr[2], xi[2], A.x, A.y);
+      cmul(xr[3], xi[3], AB.x, AB.y);
+    }
+    net4(xr, xi);
+  }
+  template <int P>
+  __device__ static __forceinline__ void inv_pass(double (&xr)[E], double (&xi)[E], const double2 *tws, int t) {
+    inet4(xr, xi);
+    if constexpr (P == 0) {
+      cmulc(xr[1], xi[1], C8, S8);
+      cmulc(xr[2], xi[2], R2, R2);
+      cmulc(xr[3], xi[3], S8, C8);
+    } else {
+      const double2 *w = tws + tw_off(P) + 3 * block<P>(t);
+      const double2 B = w[0], A = w[1], AB = w[2];
+      cmulc(xr[1], xi[1], B.x, B.y);
+      cmulc(xr[2], xi[2], A.x, A.y);
+      cmulc(xr[3], xi[3], AB.x, AB.y);
+    }
+  }
+  // P0 <-> P1 and P2 <-> P3 (an involution): register bit 1 <-> lane bit 5, register bit 0 <-> lane bit 4
+  __device__ static __forceinline__ void perm(double (&xr)[E], double (&xi)[E]) {
+    swap_lane_bit<5>(xr[0], xr[2]);
+    swap_lane_bit<5>(xi[0], xi[2]);
+    swap_lane_bit<5>(xr[1], xr[3]);
+    swap_lane_bit<5>(xi[1], xi[3]);
+    swap_lane_bit<4>(xr[0], xr[1]);
+    swap_lane_bit<4>(xi[0], xi[1]);
+    swap_lane_bit<4>(xr[2], xr[3]);
+    swap_lane_bit<4>(xi[2], xi[3]);
+  }
+  OMR_HD static constexpr int swz(int S, int j) {
+    return S == 0 ? slot_xf(j) : S == 1 ? slot_xi(j) : S == 2 ? slot_wf(j) : slot_wi(j);
+  }
+  // Slot of register e of thread t in layout P under swizzle S, as base(t) ^ xk(e) + ak(e): the
+  // swizzles and layouts are linear over GF(2), so slot = swz(idx(P, t, 0)) ^ swz(idx(P, 0, e));
+  // the bits of the second term that base(t) never sets are added as an immediate offset, the
+  // rest (at most one distinct value here) is one XOR: two address registers per side.
+  OMR_HD static constexpr int base_mask(int S, int P) {
+    int m = 0;
+    for (int t = 0; t < T; ++t) m |= swz(S, idx(P, t, 0));
+    return m;
+  }
+  template <int S, int P>
+  __device__ static __forceinline__ int slot_of(int base, int e) {
+    constexpr int M0 = base_mask(S, P);
+    const int k = swz(S, idx(P, 0, e));
+    return (k & M0 ? base ^ (k & M0) : base) + (k & ~M0);
+  }
+  // LDS exchange PF -> PT through buf (1024 double2) with swizzle S; CROSS: workgroup barrier
+  // between the writes and the reads (a cross-wave exchange), else wave-level ordering
+  template <int PF, int PT, int S, bool CROSS>
+  __device__ static __forceinline__ void exchange(double (&xr)[E], double (&xi)[E], double2 *buf, int t) {
+    const int bw = swz(S, idx(PF, t, 0)), br = swz(S, idx(PT, t, 0));
+#pragma unroll
+    for (int e = 0; e < E; ++e) buf[slot_of<S, PF>(bw, e)] = make_double2(xr[e], xi[e]);
+    if constexpr (CROSS) {
+      __syncthreads();
+    } else {
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+      __builtin_amdgcn_wave_barrier();
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    }
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const double2 v = buf[slot_of<S, PT>(br, e)];
+      xr[e] = v.x;
+      xi[e] = v.y;
+    }
+    __builtin_amdgcn_wave_barrier();  // the next writes stay below these reads (in-order LDS per wave)
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  }
+  // forward: in P0 layout (point idx(0, t, e)), out P4 layout; X: this transform's cross-wave
+  // buffer, W: the wave-local buffer
+  __device__ static __forceinline__ void fwd(double (&xr)[E], double (&xi)[E], double2 *X, double2 *W,
+                                             const double2 *tws, int t) {
+    fwd_pass<0>(xr, xi, tws, t);
+    perm(xr, xi);
+    fwd_pass<1>(xr, xi, tws, t);
+    exchange<1, 2, 0, true>(xr, xi, X, t);
+    fwd_pass<2>(xr, xi, tws, t);
+    perm(xr, xi);
+    fwd_pass<3>(xr, xi, tws, t);
+    exchange<3, 4, 2, false>(xr, xi, W, t);
+    fwd_pass<4>(xr, xi, tws, t);
+  }
+  // unscaled inverse (x 1024; the keys carry 1/1024): in P4 layout, out P0 layout
+  __device__ static __forceinline__ void inv(double (&xr)[E], double (&xi)[E], double2 *X, double2 *W,
+                                             const double2 *tws, int t) {
+    inv_pass<4>(xr, xi, tws, t);
+    exchange<4, 3, 3, false>(xr, xi, W, t);
+    inv_pass<3>(xr, xi, tws, t);
+    perm(xr, xi);
+    inv_pass<2>(xr, xi, tws, t);
+    exchange<2, 1, 1, true>(xr, xi, X, t);
+    inv_pass<1>(xr, xi, tws, t);
+    perm(xr, xi);
+    inv_pass<0>(xr, xi, tws, t);
+  }
+};
+
+constexpr double LIMB = 33554432.0;  // 2^25: key = lo + 2^25 hi
+
+// BSK2 rows (canonical u64 [670][12][2][2048]) -> FFT-domain limbs, x 1/1024:
+// out double2 [670][12][2 out][2 limb][1024] at position 4 t + e (Fft1024's P4 layout).
+__global__ __launch_bounds__(256) void key_to_fft2_kernel(const uint64_t *__restrict__ in, double2 *__restrict__ out,
+                                                          size_t npoly, const double2 *__restrict__ twg) {
+  using F = Fft1024;
+  using M = Mod<2>;
+  __shared__ double2 tws[F::TW_LEN];
+  __shared__ double2 X[F::n], W[F::n];
+  const int t = threadIdx.x;
+  const size_t poly = blockIdx.x;
+  if (poly >= npoly) return;
+  for (int j = t; j < F::TW_LEN; j += F::T) tws[j] = twg[j];
+  const uint64_t *src = in + poly * N2;
+  double lr[2][F::E], li[2][F::E];  // [limb][point]
+#pragma unroll
+  for (int e = 0; e < F::E; ++e) {
+    const int j = F::idx(0, t, e);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const double k = from_u64<M>(src[j + h * F::n]);
+      const double hi = rint(k * (1.0 / LIMB));
+      const double lo = __fma_rn(-hi, LIMB, k);
+      (h ? li : lr)[0][e] = lo;
+      (h ? li : lr)[1][e] = hi;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int l = 0; l < 2; ++l) {
+    F::fwd(lr[l], li[l], X, W, tws, t);
+    __syncthreads();  // X is reused by the next limb's exchange
+    double2 *dst = out + (poly * 2 + l) * F::n + 4 * t;
+#pragma unroll
+    for (int e = 0; e < F::E; ++e) dst[e] = make_double2(lr[l][e] * (1.0 / F::n), li[l][e] * (1.0 / F::n));
+  }
+}
+
+// Level-2 blind rotation (BlindRotationKey::blind_rotate, detector.rs:623) on the exact FFT: one
+// 256-thread workgroup per message, ACC in registers (P0 layout: coefficients j and j + 1024 of the
+// thread's 4 points), output the coefficient-domain rotation u64 [2][2048] (trace_kernel follows).
+// Per CMUX step: stage ACC_p in LDS, digits of (X^a - 1) * ACC_p (the NTT kernels' Digits2), and
+// for each digit a forward transform and the multiply-accumulate into the four (output, limb)
+// spectra with the key row, which is loaded one digit ahead; then the four inverses, rounding,
+// limb recombination mod q2 and the accumulator update. Cross-wave LDS uses alternate X1, X0 in a
+// fixed order (staging mask X1, mask digits X0 X1 X0 X1 X0 X1, staging body X0, body digits X1 ..
+// X0, inverses X1 X0 X1 X0), so no use needs a trailing barrier (the rule of cmux_step3).
+// mode 0: then hom_trace (detector.rs:626-639) with the accumulator re-laid out for the trace's
+// NTTs, output the NttRlweCiphertext; mode 1: the coefficient-domain rotation (stage tests).
+__global__ __launch_bounds__(256, 2) void br2f_kernel(const uint32_t *__restrict__ lwe_int,
+                                                      const double2 *__restrict__ bskf,
+                                                      const double2 *__restrict__ twg, const double *__restrict__ tk,
+                                                      DeviceTables tb, uint64_t *__restrict__ out, int mode) {
+  using F = Fft1024;
+  using M = Mod<2>;
+  using DG = Digits2;
+  constexpr int E = F::E, NN = N2;
+  static_assert(F::TW_LEN <= F::n, "the twiddle table's LDS doubles as the trace's NTT table");
+  __shared__ double2 tws[F::n];
+  __shared__ double2 lds2[3][F::n];  // X0, X1, W; the trace's 3 N2 doubles afterwards
+  double2(&Xb)[2][F::n] = *reinterpret_cast<double2(*)[2][F::n]>(&lds2[0][0]);
+  double2 *W = lds2[2];
+  const int t = threadIdx.x;
+  const uint32_t *lwe = lwe_int + (size_t)blockIdx.x * (NI + 1);
+  for (int j = t; j < F::TW_LEN; j += F::T) tws[j] = twg[j];
+  // ACC = (0, X^{-b} * LUT2): ac[p][h][e] = coefficient idx(0, t, e) + 1024 h of poly p
+  double ac[2][2][E];
+  {
+    const int b = (int)lwe[NI];
+    const int rr = (2 * NN - (b % (2 * NN))) % (2 * NN);
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        ac[0][h][e] = 0.0;
+        ac[1][h][e] = canon_small<M>(rot_read<NN>(tb.lut2, F::idx(0, t, e) + F::n * h, rr));
+      }
+  }
+  __syncthreads();
+  // key row: thread t's 4 points of each (output, limb) block, for the digits in issue order. The
+  // output-A blocks of the next digit are loaded one digit ahead (in flight across its transform);
+  // OMR_FULLROW loads the output-B blocks ahead too, otherwise they are loaded after the transform
+  // (in flight across output A's multiply-accumulate): 32 VGPRs fewer across the transform.
+  double2 ka[2][E], kb[2][E];
+  auto load_half = [&](double2 (&k)[2][E], const double2 *row, int o) {
+#pragma unroll
+    for (int l = 0; l < 2; ++l)
+#pragma unroll
+      for (int e = 0; e < E; ++e) k[l][e] = row[(o * 2 + l) * F::n + 4 * t + e];
+  };
+  constexpr size_t ROW = 4 * F::n;  // double2 per GGSW row
+#pragma unroll 1
+  for (int i = 0; i < NI; ++i) {
+    const int a = (int)__builtin_amdgcn_readfirstlane(lwe[i]) & (2 * NN - 1);
+    if (a == 0) continue;  // (X^0 - 1) * ACC = 0
+#ifdef OMR_ABL_KEYHOT
+    const double2 *step = bskf + (size_t)(i & 1) * 2 * D2 * ROW;
+#else
+    const double2 *step = bskf + (size_t)i * 2 * D2 * ROW;
+#endif
+    load_half(ka, step, 0);
+#ifdef OMR_FULLROW
+    load_half(kb, step, 1);
+#endif
+    double sr[2][2][E], si[2][2][E];  // [output][limb] spectra
+#pragma unroll
+    for (int o = 0; o < 2; ++o)
+#pragma unroll
+      for (int l = 0; l < 2; ++l)
+#pragma unroll
+        for (int e = 0; e < E; ++e) sr[o][l][e] = si[o][l][e] = 0.0;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      uint32_t pk[2][E][DG::DW];  // [coefficient j / j + 1024][point] digit words
+      {  // digits of (X^a - 1) * ACC_p, staged in X1 (mask) / X0 (body)
+        double *st = reinterpret_cast<double *>(Xb[p == 0 ? 1 : 0]);
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int e = 0; e < E; ++e) st[F::slot_stage(F::idx(0, t, e) + F::n * h)] = ac[p][h][e];
+        __syncthreads();
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int e = 0; e < E; ++e) {
+            const uint32_t u = (uint32_t)(F::idx(0, t, e) + F::n * h - a) & (2 * NN - 1);
+            const double v = st[F::slot_stage(u & (NN - 1))];
+            const uint32_t vh = (uint32_t)(__builtin_bit_cast(uint64_t, v) >> 32) ^ ((u & NN) << (31 - 11));
+            const double rot = __builtin_bit_cast(double, (__builtin_bit_cast(uint64_t, v) & 0xffffffffull) |
+                                                              ((uint64_t)vh << 32));
+            DG::pack(canon_small<M>(rot - ac[p][h][e]), pk[h][e]);
+            // keep the words as integers (not the doubles they come from) across the digit loop
+            asm volatile("" : "+v"(pk[h][e][0]), "+v"(pk[h][e][1]));
+          }
+        __builtin_amdgcn_wave_barrier();
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+      }
+      // digits in issue order g = 2 j + w: digit j + 3 w sits in word w at field j, so the word is
+      // chosen at compile time; its GGSW row is p D2 + j + 3 w. Cross-wave buffers: mask digits X0,
+      // X1, ..., body digits X1, X0, ... (X_{(w + p) & 1}).
+#pragma unroll 1
+      for (int j = 0; j < D2 / 2; ++j) {
+#pragma unroll
+        for (int w = 0; w < 2; ++w) {
+          double xr[E], xi[E];
+#pragma unroll
+          for (int e = 0; e < E; ++e) {
+            xr[e] = (double)((int)__builtin_amdgcn_ubfe(pk[0][e][w], 7 * j, j == 2 ? 8 : 7) - 64);
+            xi[e] = (double)((int)__builtin_amdgcn_ubfe(pk[1][e][w], 7 * j, j == 2 ? 8 : 7) - 64);
+          }
+          const double2 *row = step + (size_t)(p * D2 + j + 3 * w) * ROW;
+          // the next digit's row in issue order (the last digit reloads its own: harmless)
+          const int nx = w == 0 ? p * D2 + j + 3 : (j + 1 < D2 / 2 ? p * D2 + j + 1 : (p == 0 ? D2 : 2 * D2 - 1));
+          const double2 *next = step + (size_t)nx * ROW;
+          F::fwd(xr, xi, Xb[(w + p) & 1], W, tws, t);
+#ifndef OMR_FULLROW
+          load_half(kb, row, 1);
+#endif
+#pragma unroll
+          for (int o = 0; o < 2; ++o) {
+#pragma unroll
+            for (int l = 0; l < 2; ++l)
+#pragma unroll
+              for (int e = 0; e < E; ++e) {
+                const double2 kv = o ? kb[l][e] : ka[l][e];
+                sr[o][l][e] = __fma_rn(xr[e], kv.x, __fma_rn(-xi[e], kv.y, sr[o][l][e]));
+                si[o][l][e] = __fma_rn(xr[e], kv.y, __fma_rn(xi[e], kv.x, si[o][l][e]));
+              }
+            if (o == 0) load_half(ka, next, 0);
+#ifdef OMR_FULLROW
+            if (o == 1) load_half(kb, next, 1);
+#endif
+          }
+        }
+      }
+    }
+    // inverses (X1, X0, X1, X0), rounding to the exact limb products, recombination mod q2
+#pragma unroll
+    for (int o = 0; o < 2; ++o) {
+#pragma unroll
+      for (int l = 0; l < 2; ++l) F::inv(sr[o][l], si[o][l], Xb[1 - l], W, tws, t);
+#pragma unroll
+      for (int e = 0; e < E; ++e)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const double lo = rint(h ? si[o][0][e] : sr[o][0][e]);
+          const double hi = rint(h ? si[o][1][e] : sr[o][1][e]) * LIMB;  // exact (|P_hi| < 2^45)
+          ac[o][h][e] = canon<M>(ac[o][h][e] + red<M>(hi) + lo);
+        }
+    }
+  }
+  uint64_t *o = out + (size_t)blockIdx.x * 2 * NN;
+  if (mode == 1) {
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int e = 0; e < E; ++e) o[p * NN + F::idx(0, t, e) + F::n * h] = to_u64<M>(ac[p][h][e]);
+    return;
+  }
+  // hom_trace on the accumulator in the trace NTTs' coefficient layout (t + 256 e, 8 per thread)
+  double *xch = reinterpret_cast<double *>(&lds2[0][0]);  // 3 N2 doubles
+  double *tw = reinterpret_cast<double *>(tws);           // N2 doubles
+  __syncthreads();  // the last inverse's reads are done everywhere
+#pragma unroll
+  for (int p = 0; p < 2; ++p)
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int e = 0; e < E; ++e) xch[p * NN + F::idx(0, t, e) + F::n * h] = ac[p][h][e];
+  __syncthreads();
+  double acc0[BR2_E], acc1[BR2_E];
+#pragma unroll
+  for (int e = 0; e < BR2_E; ++e) {
+    acc0[e] = xch[t + e * BR2_T];
+    acc1[e] = xch[NN + t + e * BR2_T];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int e = 0; e < BR2_E; ++e) {
+    tw[t + e * BR2_T] = tb.tw2[t + e * BR2_T];
+    xch[2 * NN + t + e * BR2_T] = tb.itw2[t + e * BR2_T];
+  }
+  __syncthreads();
+  hom_trace_store(acc0, acc1, xch, tw, xch + 2 * NN, tk, tb, o, t);
+}
+
+}  // namespace omr

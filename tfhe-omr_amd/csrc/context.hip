@@ -13,6 +13,7 @@
 #include <string>
 #include <vector>
 
+#include "br2_fft.hpp"
 #include "detect_kernels.hpp"
 #include "encode_kernels.hpp"
 #include "latency_kernels.hpp"
@@ -117,6 +118,38 @@ std::vector<double2> fft_twiddles() {
   return tw;
 }
 
+// Fft1024 twiddles (br2_fft.hpp): pass p = 1..4, block hi -> (B, A, AB) at tw_off(p) + 3 hi, with
+// A = W(2p, hi), B = W(2p + 1, 2 hi) of the tree with n = 1024 (eps(0, 0) = n, w = e^{i pi / 2n});
+// each entry an exact angle evaluated in long double and rounded once.
+std::vector<double2> fft2_twiddles() {
+  const int L = 10, n = 1 << L;
+  std::vector<std::vector<long>> half(L);
+  std::vector<long> eps{n};
+  for (int s = 0; s < L; ++s) {
+    std::vector<long> next;
+    for (long e : eps) {
+      half[s].push_back(e / 2);
+      next.push_back((e / 2) % (4 * n));
+      next.push_back((e / 2 + 2 * n) % (4 * n));
+    }
+    eps.swap(next);
+  }
+  auto at = [&](long h) {
+    const long double ang = 3.14159265358979323846264338327950288L * (long double)(h % (8 * n)) / (long double)(2 * n);
+    return make_double2((double)cosl(ang), (double)sinl(ang));
+  };
+  std::vector<double2> tw(Fft1024::TW_LEN);
+  int off = 0;
+  for (int p = 1; p <= 4; ++p)
+    for (int hi = 0; hi < (1 << (2 * p)); ++hi) {
+      const long a = half[2 * p][hi], b = half[2 * p + 1][2 * hi];
+      tw[off++] = at(b);
+      tw[off++] = at(a);
+      tw[off++] = at(a + b);
+    }
+  return tw;
+}
+
 }  // namespace
 
 #ifndef OMR_DEFAULT_LATENCY_MAX
@@ -128,7 +161,9 @@ struct omr_ctx {
   hipStream_t stream = nullptr;
   double2 *bsk1f = nullptr;  // level-1 FFT-domain keys [512][8][2][512] complex, x 1/512
   double2 *fft1 = nullptr;   // level-1 FFT twiddles
-  double *bsk2 = nullptr, *tk = nullptr;
+  double *bsk2 = nullptr, *tk = nullptr;  // BSK2 NTT domain (latency kernels), trace key
+  double2 *bsk2f = nullptr;                // BSK2 as FFT-domain 25-bit limbs (br2f_kernel), x 1/1024
+  double2 *fft2 = nullptr;                 // Fft1024 twiddles
   uint32_t *kskb = nullptr;  // int8 limbs of the KSK, [1024][4][672][32] (matrix-core key switch)
   double *tables = nullptr;  // tw1 itw1 tw2 itw2 lut1 lut2 tw2c
   uint16_t *trace_tabs = nullptr;
@@ -287,6 +322,21 @@ omr_status convert_keys_cmux(const uint64_t *host, size_t npoly, double *dev, do
   return OMR_OK;
 }
 
+omr_status convert_keys_fft2(const uint64_t *host, size_t npoly, double2 *dev, const double2 *tw, hipStream_t st) {
+  const size_t chunk = 4096;  // polynomials per upload
+  uint64_t *tmp = nullptr;
+  HIP_TRY(hipMalloc(&tmp, chunk * N2 * sizeof(uint64_t)));
+  for (size_t p0 = 0; p0 < npoly; p0 += chunk) {
+    const size_t n = std::min(chunk, npoly - p0);
+    HIP_TRY(hipMemcpyAsync(tmp, host + p0 * N2, n * N2 * sizeof(uint64_t), hipMemcpyDefault, st));
+    key_to_fft2_kernel<<<n, Fft1024::T, 0, st>>>(tmp, dev + p0 * 2 * Fft1024::n, n, tw);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(st));
+  }
+  dev_free(tmp);
+  return OMR_OK;
+}
+
 omr_status convert_keys_fft1(const uint32_t *host, size_t npoly, double2 *dev, const double2 *tw,
                              hipStream_t st) {
   const size_t chunk = 4096;
@@ -402,10 +452,20 @@ omr_status launch_br2(omr_ctx *c, size_t n, const uint32_t *lwe_int, uint64_t *o
     if ((s = launch_br2x(c, n, lwe_int, out, st, &two_cu)) != OMR_OK) return s;
     if (!two_cu) br2l_kernel<<<(unsigned)n, BR2L_T, 0, st>>>(lwe_int, c->bsk2, c->tb, out);
     split_trace = true;
-  } else if (split_trace && mode == 0) {
-    br2_trace_kernel<<<(unsigned)n, BR2_T, 0, st>>>(lwe_int, c->bsk2, c->tk, c->tb, out, 1);
   } else {
-    br2_trace_kernel<<<(unsigned)n, BR2_T, 0, st>>>(lwe_int, c->bsk2, c->tk, c->tb, out, mode);
+#ifdef OMR_L2_NTT
+    if (split_trace && mode == 0) {
+      br2_trace_kernel<<<(unsigned)n, BR2_T, 0, st>>>(lwe_int, c->bsk2, c->tk, c->tb, out, 1);
+    } else {
+      br2_trace_kernel<<<(unsigned)n, BR2_T, 0, st>>>(lwe_int, c->bsk2, c->tk, c->tb, out, mode);
+    }
+#else
+    if (split_trace && mode == 0) {
+      br2f_kernel<<<(unsigned)n, Fft1024::T, 0, st>>>(lwe_int, c->bsk2f, c->fft2, c->tk, c->tb, out, 1);
+    } else {
+      br2f_kernel<<<(unsigned)n, Fft1024::T, 0, st>>>(lwe_int, c->bsk2f, c->fft2, c->tk, c->tb, out, mode);
+    }
+#endif
   }
   HIP_TRY(hipGetLastError());
   if (mid) HIP_TRY(hipEventRecord(mid, st));
@@ -502,9 +562,15 @@ extern "C" omr_status omr_ctx_create(const omr_detection_key_view *key, int devi
   if (hipMemcpy(c->fft1, ftw.data(), ftw.size() * sizeof(double2), hipMemcpyHostToDevice) != hipSuccess)
     return fail(set_error(OMR_ERR_DEVICE, "omr_ctx_create: table upload"));
   c->tb.fft1 = c->fft1;
+  const auto ftw2 = fft2_twiddles();
+  if (hipMalloc(&c->fft2, ftw2.size() * sizeof(double2)) != hipSuccess)
+    return fail(set_error(OMR_ERR_OUT_OF_MEMORY, "omr_ctx_create: tables"));
+  if (hipMemcpy(c->fft2, ftw2.data(), ftw2.size() * sizeof(double2), hipMemcpyHostToDevice) != hipSuccess)
+    return fail(set_error(OMR_ERR_DEVICE, "omr_ctx_create: table upload"));
   // keys
   if (hipMalloc(&c->bsk1f, BSK1_ELEMS / 2 * sizeof(double2)) != hipSuccess ||
       hipMalloc(&c->bsk2, BSK2_ELEMS * sizeof(double)) != hipSuccess ||
+      hipMalloc(&c->bsk2f, BSK2_ELEMS * sizeof(double2)) != hipSuccess ||
       hipMalloc(&c->tk, TK_ELEMS * sizeof(double)) != hipSuccess ||
       hipMalloc(&c->kskb, KSKB_WORDS * sizeof(uint32_t)) != hipSuccess)
     return fail(set_error(OMR_ERR_OUT_OF_MEMORY, "omr_ctx_create: key buffers"));
@@ -514,6 +580,7 @@ extern "C" omr_status omr_ctx_create(const omr_detection_key_view *key, int devi
     return fail(st);
   if ((st = convert_keys_cmux(key->bsk2, BSK2_ELEMS / N2, c->bsk2, ninv2, c->tb.tw2c, c->stream)) != OMR_OK)
     return fail(st);
+  if ((st = convert_keys_fft2(key->bsk2, BSK2_ELEMS / N2, c->bsk2f, c->fft2, c->stream)) != OMR_OK) return fail(st);
   if ((st = convert_keys<2, uint64_t, double>(key->trace_key, TK_ELEMS / N2, c->tk, 1.0, c->tb.tw2,
                                               c->stream)) != OMR_OK)
     return fail(st);
@@ -541,6 +608,8 @@ extern "C" void omr_ctx_destroy(omr_ctx *c) {
   dev_free(c->bsk1f);
   dev_free(c->fft1);
   dev_free(c->bsk2);
+  dev_free(c->bsk2f);
+  dev_free(c->fft2);
   dev_free(c->tk);
   dev_free(c->kskb);
   dev_free(c->tables);
