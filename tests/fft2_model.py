@@ -71,6 +71,11 @@ TW_OFF = {1: 0, 2: 3 * 4, 3: 3 * (4 + 16), 4: 3 * (4 + 16 + 64)}
 TW_LEN = 3 * (4 + 16 + 64 + 256)
 
 
+def tw_addr(p, t, k):
+    """Table slot (double2) of twiddle k (0 B, 1 A, 2 AB) of thread t's block in pass p."""
+    return TW_OFF[p] + 3 * tw_index(p, t) + k
+
+
 def twiddle_table():
     tab = np.zeros(TW_LEN, np.complex128)
     for p in range(1, 5):

@@ -166,6 +166,25 @@ def test_latency_level2_variants_match_throughput(real):
             assert (dec[0] == 1) == mask[m] and not dec[1:].any()
 
 
+def test_level2_throughput_small_batches(real):
+    """The throughput level-2 kernel (br2f_kernel; the -DOMR_L2_PAIR build's br2fp_kernel, two
+    messages per workgroup, has an odd tail here) at batches of 5 and 6 messages against the
+    latency kernels (oracle-checked NTT path), rotation and rotation + trace."""
+    _, det, _ = real
+    for n in (5, 6):
+        mask = np.zeros(n, dtype=bool)
+        mask[1::3] = True
+        ca, cb = PL.mixed_clues(mask, seed=700 + n)
+        fl = det.first_level(ca, cb)
+        det.set_latency_threshold(0)
+        try:
+            thr_br, thr_tr = det.blind_rotate_level2(fl), det.second_level(fl)
+        finally:
+            det.set_latency_threshold(64)
+        assert np.array_equal(thr_br, det.blind_rotate_level2(fl))
+        assert np.array_equal(thr_tr, det.second_level(fl))
+
+
 def test_encode_golden(structured):
     det, _ = structured
     z = np.load(os.path.join(GOLDEN, "encode.npz"))

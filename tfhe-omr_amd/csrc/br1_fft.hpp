@@ -140,11 +140,6 @@ __device__ __forceinline__ void vm_wait_row_in_flight() {  // s_waitcnt vmcnt(KR
 __device__ __forceinline__ void vm_wait_all() {  // s_waitcnt vmcnt(0)
   __builtin_amdgcn_s_waitcnt((0x7 << 4) | (0xF << 8));
 }
-__device__ __forceinline__ void wg_barrier_lds() {  // LDS reads/writes done, then s_barrier
-  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
-  __builtin_amdgcn_s_barrier();
-  __atomic_signal_fence(__ATOMIC_SEQ_CST);
-}
 
 // One CMUX step with LDS-staged key rows. q0 = first global row of this step; rows q0..q0+7 are
 // consumed, the next step's first row is prefetched on the way. xch: the wave's exchange buffer

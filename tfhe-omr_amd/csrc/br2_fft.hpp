@@ -184,7 +184,7 @@ struct Fft1024 {
 #pragma unroll
     for (int e = 0; e < E; ++e) buf[slot_of<S, PF>(bw, e)] = make_double2(xr[e], xi[e]);
     if constexpr (CROSS) {
-      __syncthreads();
+      wg_barrier_lds();  // global loads (the next key blocks) stay in flight
     } else {
       __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
       __builtin_amdgcn_wave_barrier();
@@ -310,8 +310,9 @@ __global__ __launch_bounds__(256, 2) void br2f_kernel(const uint32_t *__restrict
   __syncthreads();
   // key row: thread t's 4 points of each (output, limb) block, for the digits in issue order. The
   // output-A blocks of the next digit are loaded one digit ahead (in flight across its transform);
-  // OMR_FULLROW loads the output-B blocks ahead too, otherwise they are loaded after the transform
-  // (in flight across output A's multiply-accumulate): 32 VGPRs fewer across the transform.
+  // the output-B blocks are loaded after the transform (in flight across output A's
+  // multiply-accumulate): 32 VGPRs fewer across the transform. Loading them earlier (before or
+  // inside the transform) measured 43-50 % slower (profiles/r03/level2_experiments.log).
   double2 ka[2][E], kb[2][E];
   auto load_half = [&](double2 (&k)[2][E], const double2 *row, int o) {
 #pragma unroll
@@ -324,15 +325,8 @@ __global__ __launch_bounds__(256, 2) void br2f_kernel(const uint32_t *__restrict
   for (int i = 0; i < NI; ++i) {
     const int a = (int)__builtin_amdgcn_readfirstlane(lwe[i]) & (2 * NN - 1);
     if (a == 0) continue;  // (X^0 - 1) * ACC = 0
-#ifdef OMR_ABL_KEYHOT
-    const double2 *step = bskf + (size_t)(i & 1) * 2 * D2 * ROW;
-#else
     const double2 *step = bskf + (size_t)i * 2 * D2 * ROW;
-#endif
     load_half(ka, step, 0);
-#ifdef OMR_FULLROW
-    load_half(kb, step, 1);
-#endif
     double sr[2][2][E], si[2][2][E];  // [output][limb] spectra
 #pragma unroll
     for (int o = 0; o < 2; ++o)
@@ -349,7 +343,7 @@ __global__ __launch_bounds__(256, 2) void br2f_kernel(const uint32_t *__restrict
         for (int h = 0; h < 2; ++h)
 #pragma unroll
           for (int e = 0; e < E; ++e) st[F::slot_stage(F::idx(0, t, e) + F::n * h)] = ac[p][h][e];
-        __syncthreads();
+        wg_barrier_lds();
 #pragma unroll
         for (int h = 0; h < 2; ++h)
 #pragma unroll
@@ -384,9 +378,7 @@ __global__ __launch_bounds__(256, 2) void br2f_kernel(const uint32_t *__restrict
           const int nx = w == 0 ? p * D2 + j + 3 : (j + 1 < D2 / 2 ? p * D2 + j + 1 : (p == 0 ? D2 : 2 * D2 - 1));
           const double2 *next = step + (size_t)nx * ROW;
           F::fwd(xr, xi, Xb[(w + p) & 1], W, tws, t);
-#ifndef OMR_FULLROW
           load_half(kb, row, 1);
-#endif
 #pragma unroll
           for (int o = 0; o < 2; ++o) {
 #pragma unroll
@@ -398,9 +390,6 @@ __global__ __launch_bounds__(256, 2) void br2f_kernel(const uint32_t *__restrict
                 si[o][l][e] = __fma_rn(xr[e], kv.y, __fma_rn(xi[e], kv.x, si[o][l][e]));
               }
             if (o == 0) load_half(ka, next, 0);
-#ifdef OMR_FULLROW
-            if (o == 1) load_half(kb, next, 1);
-#endif
           }
         }
       }
@@ -455,6 +444,209 @@ __global__ __launch_bounds__(256, 2) void br2f_kernel(const uint32_t *__restrict
   }
   __syncthreads();
   hom_trace_store(acc0, acc1, xch, tw, xch + 2 * NN, tk, tb, o, t);
+}
+
+
+// Level-2 blind rotation on the exact FFT, two messages per 512-thread workgroup (br2fp; build
+// variant -DOMR_L2_PAIR, not the production path): br2f_kernel streams 768 KB of FFT-domain key
+// per CMUX step and message from L2. Here the two 256-thread groups of a workgroup each transform
+// their own message's digits (group g, message g) and swap the spectra through LDS (S_g), so every
+// thread multiplies BOTH messages' spectra by the key blocks of ONE output (group g: output g, both
+// limbs): each key byte is read once per pair of messages, 384 KB per message-step. Group g owns
+// output g's accumulator of both messages, runs their four inverse transforms and recombines
+// them; the digits of message g are taken from accumulators staged in LDS by their owner. Same
+// rows, digits, transforms and rounding as br2f_kernel: bit-identical output. Measured 787 ms vs
+// 667 ms per 16,384 messages (profiles/r03/level2_experiments.log): the key stream is not what
+// binds br2f (an L1-resident key saves 12 %), and the extra workgroup-wide barrier per digit
+// across 8 waves costs more than the halved key traffic saves.
+//
+// Per digit: transform (X_g, one workgroup barrier; W_g wave-local), spectrum to S_g, barrier,
+// other spectrum from S_{1-g}, multiply-accumulate. A buffer is rewritten only after a barrier
+// that follows every read of it (the inverses alternate X_g and S_g).
+// LDS: twiddles 16 KB + (X, W, S) x 2 groups 96 KB + staging 32 KB = 144 KB, one workgroup per
+// CU (8 waves: two per SIMD, as two single-message workgroups).
+constexpr int BR2P_T = 512;
+__global__ __launch_bounds__(BR2P_T, 1) void br2fp_kernel(const uint32_t *__restrict__ lwe_int, size_t nmsg,
+                                                          const double2 *__restrict__ bskf,
+                                                          const double2 *__restrict__ twg, const double *__restrict__ tk,
+                                                          DeviceTables tb, uint64_t *__restrict__ out, int mode) {
+  using F = Fft1024;
+  using M = Mod<2>;
+  using DG = Digits2;
+  constexpr int E = F::E, NN = N2;
+  __shared__ double2 tws[F::n];
+  __shared__ double2 grp[2][3][F::n];      // per group: X, W, S
+  __shared__ double stage[2][NN];          // [message][coefficient] of one output poly
+  const int g = __builtin_amdgcn_readfirstlane(threadIdx.x >> 8), t = threadIdx.x & 255;
+  // staging slot of coefficient idx(0, t, e) + 1024 h: sb + idx(0, 0, e) + 1024 h (slot_stage only
+  // flips bit 4 by bit 6, both thread bits)
+  const int sb = F::slot_stage(F::idx(0, t, 0));
+  double2 *X = grp[g][0], *W = grp[g][1], *S = grp[g][2];
+  const double2 *So = grp[g ^ 1][2];
+  // messages of this workgroup: k = 0 "mine" (message g), k = 1 the other group's
+  const size_t m0 = 2 * (size_t)blockIdx.x;
+  const size_t mk[2] = {min(m0 + g, nmsg - 1), min(m0 + (g ^ 1), nmsg - 1)};
+  const uint32_t *lwe0 = lwe_int + min(m0, nmsg - 1) * (NI + 1);
+  const uint32_t *lwe1 = lwe_int + min(m0 + 1, nmsg - 1) * (NI + 1);
+  for (int j = threadIdx.x; j < F::TW_LEN; j += BR2P_T) tws[j] = twg[j];
+  // output g of message (g ^ k): ac[k][h][e] = coefficient idx(0, t, e) + 1024 h
+  double ac[2][2][E];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int b = (int)lwe_int[mk[k] * (NI + 1) + NI];
+    const int rr = (2 * NN - (b % (2 * NN))) % (2 * NN);
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int e = 0; e < E; ++e)
+        ac[k][h][e] = g == 0 ? 0.0 : canon_small<M>(rot_read<NN>(tb.lut2, F::idx(0, t, e) + F::n * h, rr));
+  }
+  __syncthreads();
+  double2 kv[2][E];  // this group's key blocks (output g, limbs 0 / 1) of the next digit in issue order
+  auto load_key = [&](const double2 *row) {
+#pragma unroll
+    for (int l = 0; l < 2; ++l)
+#pragma unroll
+      for (int e = 0; e < E; ++e) kv[l][e] = row[(g * 2 + l) * F::n + 4 * t + e];
+  };
+  constexpr size_t ROW = 4 * F::n;  // double2 per GGSW row
+#pragma unroll 1
+  for (int i = 0; i < NI; ++i) {
+    const int a0 = (int)__builtin_amdgcn_readfirstlane(lwe0[i]) & (2 * NN - 1);
+    const int a1 = (int)__builtin_amdgcn_readfirstlane(lwe1[i]) & (2 * NN - 1);
+    if ((a0 | a1) == 0) continue;  // (X^0 - 1) * ACC = 0 for both messages
+    const int a = g ? a1 : a0;     // wave-uniform
+    const double2 *step = bskf + (size_t)i * 2 * D2 * ROW;
+    load_key(step);
+    double sr[2][2][E], si[2][2][E];  // [message k][limb] spectra of output g
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+#pragma unroll
+      for (int l = 0; l < 2; ++l)
+#pragma unroll
+        for (int e = 0; e < E; ++e) sr[k][l][e] = si[k][l][e] = 0.0;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      uint32_t pk[2][E][DG::DW];  // digit words of (X^a - 1) * ACC_p of message g
+      // the owner (group p) stages output p of both messages; group g reads message g's
+      if (g == p) {
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int e = 0; e < E; ++e) stage[g ^ k][sb + F::idx(0, 0, e) + F::n * h] = ac[k][h][e];
+      }
+      wg_barrier_lds();
+      {
+        const double *st = stage[g];
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int e = 0; e < E; ++e) {
+            const int j = F::idx(0, t, e) + F::n * h;
+            const uint32_t u = (uint32_t)(j - a) & (2 * NN - 1);
+            const double v = st[F::slot_stage(u & (NN - 1))];
+            const uint32_t vh = (uint32_t)(__builtin_bit_cast(uint64_t, v) >> 32) ^ ((u & NN) << (31 - 11));
+            const double rot = __builtin_bit_cast(double, (__builtin_bit_cast(uint64_t, v) & 0xffffffffull) |
+                                                              ((uint64_t)vh << 32));
+            DG::pack(canon_small<M>(rot - st[sb + F::idx(0, 0, e) + F::n * h]), pk[h][e]);
+            asm volatile("" : "+v"(pk[h][e][0]), "+v"(pk[h][e][1]));
+          }
+      }
+      // digits in issue order g' = 2 j + w (digit j + 3 w: word w, field j; GGSW row p D2 + j + 3 w)
+#pragma unroll 1
+      for (int j = 0; j < D2 / 2; ++j) {
+#pragma unroll
+        for (int w = 0; w < 2; ++w) {
+          double xr[E], xi[E];
+#pragma unroll
+          for (int e = 0; e < E; ++e) {
+            xr[e] = (double)((int)__builtin_amdgcn_ubfe(pk[0][e][w], 7 * j, j == 2 ? 8 : 7) - 64);
+            xi[e] = (double)((int)__builtin_amdgcn_ubfe(pk[1][e][w], 7 * j, j == 2 ? 8 : 7) - 64);
+          }
+          const int nx = w == 0 ? p * D2 + j + 3 : (j + 1 < D2 / 2 ? p * D2 + j + 1 : (p == 0 ? D2 : 2 * D2 - 1));
+          const double2 *next = step + (size_t)nx * ROW;
+          F::fwd(xr, xi, X, W, tws, t);
+#pragma unroll
+          for (int e = 0; e < E; ++e) S[e * F::T + t] = make_double2(xr[e], xi[e]);
+          wg_barrier_lds();
+          double yr[E], yi[E];
+#pragma unroll
+          for (int e = 0; e < E; ++e) {
+            const double2 v = So[e * F::T + t];
+            yr[e] = v.x;
+            yi[e] = v.y;
+          }
+#pragma unroll
+          for (int l = 0; l < 2; ++l)
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+              const double2 k = kv[l][e];
+              sr[0][l][e] = __fma_rn(xr[e], k.x, __fma_rn(-xi[e], k.y, sr[0][l][e]));
+              si[0][l][e] = __fma_rn(xr[e], k.y, __fma_rn(xi[e], k.x, si[0][l][e]));
+              sr[1][l][e] = __fma_rn(yr[e], k.x, __fma_rn(-yi[e], k.y, sr[1][l][e]));
+              si[1][l][e] = __fma_rn(yr[e], k.y, __fma_rn(yi[e], k.x, si[1][l][e]));
+            }
+          load_key(next);  // the last digit reloads its own row: harmless
+        }
+      }
+    }
+    // inverses (X, S, X, S), rounding to the exact limb products, recombination mod q2
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+#pragma unroll
+      for (int l = 0; l < 2; ++l) F::inv(sr[k][l], si[k][l], l ? S : X, W, tws, t);
+#pragma unroll
+      for (int e = 0; e < E; ++e)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const double lo = rint(h ? si[k][0][e] : sr[k][0][e]);
+          const double hi = rint(h ? si[k][1][e] : sr[k][1][e]) * LIMB;
+          ac[k][h][e] = canon<M>(ac[k][h][e] + red<M>(hi) + lo);
+        }
+    }
+  }
+  if (mode == 1) {
+    // group g stores output g of both messages (each message's owner pair covers both outputs)
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      if (m0 + (g ^ k) >= nmsg) continue;
+      uint64_t *o = out + (m0 + (g ^ k)) * 2 * NN + g * NN;
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int e = 0; e < E; ++e) o[F::idx(0, t, e) + F::n * h] = to_u64<M>(ac[k][h][e]);
+    }
+    return;
+  }
+  // hom_trace per group on its own message: mask / body of message g in the trace layout
+  double *xfer = reinterpret_cast<double *>(&grp[0][0][0]);  // [message][output][N2] doubles, 64 KB
+  __syncthreads();  // the last inverses' reads are done everywhere
+#pragma unroll
+  for (int k = 0; k < 2; ++k)
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int e = 0; e < E; ++e) xfer[((g ^ k) * 2 + g) * NN + F::idx(0, t, e) + F::n * h] = ac[k][h][e];
+  __syncthreads();
+  double acc0[BR2_E], acc1[BR2_E];
+#pragma unroll
+  for (int e = 0; e < BR2_E; ++e) {
+    acc0[e] = xfer[(g * 2 + 0) * NN + t + e * BR2_T];
+    acc1[e] = xfer[(g * 2 + 1) * NN + t + e * BR2_T];
+  }
+  __syncthreads();
+  double *tw = reinterpret_cast<double *>(tws);  // N2 doubles
+  double *itw = &stage[0][0];                     // N2 doubles
+  for (int j = threadIdx.x; j < NN; j += BR2P_T) {
+    tw[j] = tb.tw2[j];
+    itw[j] = tb.itw2[j];
+  }
+  __syncthreads();
+  double *xch = reinterpret_cast<double *>(&grp[g][0][0]);  // 2 N2 doubles (X, W) per group
+  // (an odd tail's group 1 repeats the last message and stores the same values as group 0)
+  hom_trace_store(acc0, acc1, xch, tw, itw, tk, tb, out + mk[0] * 2 * NN, t);
 }
 
 }  // namespace omr

@@ -6,7 +6,7 @@
 // FP64 NTT-domain rows with N^-1 folded into the external-product keys, the KSK to int8 limbs)
 // and builds the LUTs (:457-503). Detector::detect (:135-166) for a batch of messages -> four
 // launches per chunk: br1f_kernel (7 blind rotations per message), sum7_kernel, ks_mfma_kernel,
-// br2_trace_kernel.
+// br2f_kernel (level-2 rotation on the exact FFT + the trace).
 #include <algorithm>
 #include <cstring>
 #include <mutex>
@@ -209,7 +209,13 @@ struct omr_ctx {
 
 #define OMR_BR1_NAME "br1f_kernel"
 #define OMR_KS_NAME "ks_mfma_kernel"
+#ifdef OMR_L2_NTT  // build variant: level 2 on the modular NTT (round-2 kernel), for A/B runs
 #define OMR_BR2_NAME "br2_trace_kernel"
+#elif defined(OMR_L2_PAIR)  // build variant: two messages per workgroup (br2fp_kernel)
+#define OMR_BR2_NAME "br2fp_kernel"
+#else
+#define OMR_BR2_NAME "br2f_kernel"
+#endif
 
 namespace {
 
@@ -459,12 +465,12 @@ omr_status launch_br2(omr_ctx *c, size_t n, const uint32_t *lwe_int, uint64_t *o
     } else {
       br2_trace_kernel<<<(unsigned)n, BR2_T, 0, st>>>(lwe_int, c->bsk2, c->tk, c->tb, out, mode);
     }
+#elif defined(OMR_L2_PAIR)
+    br2fp_kernel<<<(unsigned)((n + 1) / 2), BR2P_T, 0, st>>>(lwe_int, n, c->bsk2f, c->fft2, c->tk, c->tb, out,
+                                                             split_trace && mode == 0 ? 1 : mode);
 #else
-    if (split_trace && mode == 0) {
-      br2f_kernel<<<(unsigned)n, Fft1024::T, 0, st>>>(lwe_int, c->bsk2f, c->fft2, c->tk, c->tb, out, 1);
-    } else {
-      br2f_kernel<<<(unsigned)n, Fft1024::T, 0, st>>>(lwe_int, c->bsk2f, c->fft2, c->tk, c->tb, out, mode);
-    }
+    br2f_kernel<<<(unsigned)n, Fft1024::T, 0, st>>>(lwe_int, c->bsk2f, c->fft2, c->tk, c->tb, out,
+                                                    split_trace && mode == 0 ? 1 : mode);
 #endif
   }
   HIP_TRY(hipGetLastError());
@@ -567,6 +573,7 @@ extern "C" omr_status omr_ctx_create(const omr_detection_key_view *key, int devi
     return fail(set_error(OMR_ERR_OUT_OF_MEMORY, "omr_ctx_create: tables"));
   if (hipMemcpy(c->fft2, ftw2.data(), ftw2.size() * sizeof(double2), hipMemcpyHostToDevice) != hipSuccess)
     return fail(set_error(OMR_ERR_DEVICE, "omr_ctx_create: table upload"));
+
   // keys
   if (hipMalloc(&c->bsk1f, BSK1_ELEMS / 2 * sizeof(double2)) != hipSuccess ||
       hipMalloc(&c->bsk2, BSK2_ELEMS * sizeof(double)) != hipSuccess ||

@@ -16,6 +16,16 @@ namespace omr {
 // 32..63 of a <-> lanes 0..31 of b, v_permlane32_swap; 4: odd 16-lane rows of a <-> even rows of
 // b, v_permlane16_swap): afterwards a holds the lane-bit-0 half and lane bit LB indexes the old
 // register bit. One instruction per dword pair.
+// Workgroup barrier for LDS traffic only: this wave's LDS reads / writes are done, then s_barrier.
+// Unlike __syncthreads() (a workgroup-scope fence: s_waitcnt vmcnt(0) lgkmcnt(0)) it leaves the
+// wave's global loads in flight across the barrier (cdna_hip_programming.md, "Pipelining across
+// barriers"); callers that hand global data between waves must not use it.
+__device__ __forceinline__ void wg_barrier_lds() {
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+  __builtin_amdgcn_s_barrier();
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+}
+
 template <int LB>
 __device__ __forceinline__ void swap_lane_bit(double &a, double &b) {
   static_assert(LB == 4 || LB == 5, "lane bits 4 and 5 have swap instructions");

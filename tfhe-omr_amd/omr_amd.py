@@ -7,8 +7,10 @@ the HIP C ABI; there is no CPU fallback: if libomr_gpu.so is missing this module
 """
 from __future__ import annotations
 
+import atexit
 import ctypes as C
 import os
+import weakref
 from dataclasses import dataclass
 
 import numpy as np
@@ -348,6 +350,17 @@ class Retriever:
         return indices, self.decode_combined_payloads_and_solve(pay_cts, weights, indices)
 
 
+# Contexts still open at interpreter exit are destroyed by an atexit hook, which runs before the
+# HIP runtime's own exit-time teardown (a context freed after it faults, e.g. under rocprofv3).
+_LIVE_DETECTORS: "weakref.WeakSet[Detector]" = weakref.WeakSet()
+
+
+@atexit.register
+def _close_live_detectors():
+    for d in list(_LIVE_DETECTORS):
+        d.close()
+
+
 class Detector:
     """Detector (detector.rs:35-453) on one MI355X."""
 
@@ -362,6 +375,7 @@ class Detector:
         _check(lib().omr_ctx_create(C.byref(view), device, C.byref(h)), "omr_ctx_create")
         self._h = h
         self.device = device
+        _LIVE_DETECTORS.add(self)
 
     @classmethod
     def from_device_key(cls, d_bsk1: int, d_ksk: int, d_bsk2: int, d_trace_key: int, device: int = 0):
@@ -373,6 +387,7 @@ class Detector:
         _check(lib().omr_ctx_create(C.byref(view), device, C.byref(h)), "omr_ctx_create")
         self._h = h
         self.device = device
+        _LIVE_DETECTORS.add(self)
         return self
 
     def close(self):

@@ -25,3 +25,4 @@ for D in [int(x) for x in sys.argv[1:]] or [1, 2, 7, 64]:
     print(f"D={D}: wall {w:.2f} ms  br1 {info['first_level_ms'] - info['key_switch_ms']:.2f}  "
           f"ks {info['key_switch_ms']:.3f}  br2 {info['second_level_ms']:.2f}  trace {info['trace_ms']:.3f}  "
           f"device total {info['total_ms']:.2f}", flush=True)
+det.close()
