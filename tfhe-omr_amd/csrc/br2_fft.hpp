@@ -649,4 +649,211 @@ __global__ __launch_bounds__(BR2P_T, 1) void br2fp_kernel(const uint32_t *__rest
   hom_trace_store(acc0, acc1, xch, tw, itw, tk, tb, out + mk[0] * 2 * NN, t);
 }
 
+
+// ---- level-2 latency on the exact FFT, two CUs per message (br2xf) ---------------------------
+// The latency path's level 2 (br2x_kernel's protocol, latency_kernels.hpp) with br2f's transform:
+// workgroup 2m + r (512 threads, one per CU) owns polynomial r of message m (0 mask, 1 body) and its
+// accumulator (group 0). Per CMUX step: group 0 stages ACC_r; group g decomposes it and transforms
+// digits 3g .. 3g + 2 (one digit word per coefficient), multiply-accumulating all four (output,
+// limb) spectra with GGSW rows r D2 + 3g + h; the groups swap partials so that group g holds limb
+// g of both outputs summed over the workgroup's six digits; group g hands its output-(1 - r)
+// partial of limb g to the partner CU through global memory (sc1 stores, flag hc + 1 per executed
+// step, slot hc & 1, bounded poll: br2x's hand-off rules) and adds the partner's output-r partial;
+// group g runs the inverse of limb g (the two limbs in parallel), group 1 passes its rounded,
+// 2^25-scaled limb to group 0 through LDS and group 0 updates ACC_r. Per step and group: three
+// forward FFTs and one inverse instead of br2x's three forward NTTs and (group 0) one inverse.
+// Same digits, rows and exact rounding as br2f_kernel: bit-identical. LDS: twiddles 16 KB + per
+// group X0, X1, W (96 KB); the staging (group 0's X1), the partial swap (both groups' X0, X1) and
+// the limb hand-over (group 1's X1) alias them between barriers.
+// Global slots: xg[m][r][limb][slot][e * 256 + t] double2 (16 KB per limb and slot).
+constexpr size_t BR2XF_SLOT_D2 = 1024;  // double2 per hand-off slot: one limb spectrum (4 points x 256 threads)
+__global__ __launch_bounds__(512, 1) void br2xf_kernel(const uint32_t *__restrict__ lwe_int,
+                                                       const double2 *__restrict__ bskf,
+                                                       const double2 *__restrict__ twg, DeviceTables tb,
+                                                       double2 *xg, uint32_t *flags, int *err,
+                                                       uint64_t *__restrict__ out) {
+  using F = Fft1024;
+  using M = Mod<2>;
+  constexpr int E = F::E, NN = N2, KD = D2 / 2;
+  __shared__ double2 tws[F::n];
+  __shared__ double2 buf[2][3][F::n];  // per group: X0, X1, W
+  __shared__ int stop;
+  const int m = blockIdx.x >> 1, r = blockIdx.x & 1;
+  const int g = __builtin_amdgcn_readfirstlane(threadIdx.x >> 8), t = threadIdx.x & 255;
+  double2 *X0 = buf[g][0], *X1 = buf[g][1], *W = buf[g][2];
+  double *ST = reinterpret_cast<double *>(buf[0][1]);  // staged ACC_r (group 0's X1)
+  const uint32_t *lwe = lwe_int + (size_t)m * (NI + 1);
+  for (int j = threadIdx.x; j < F::TW_LEN; j += 512) tws[j] = twg[j];
+  double ac[2][E];  // ACC_r, group 0: coefficient idx(0, t, e) + 1024 h
+  {
+    const int b = (int)lwe[NI];
+    const int rr = (2 * NN - (b % (2 * NN))) % (2 * NN);
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int e = 0; e < E; ++e)
+        ac[h][e] = r == 1 ? canon_small<M>(rot_read<NN>(tb.lut2, F::idx(0, t, e) + F::n * h, rr)) : 0.0;
+  }
+  if (threadIdx.x == 0) stop = 0;
+  __syncthreads();
+  uint32_t *my_flag = flags + 2 * m + r, *their_flag = flags + 2 * m + (1 - r);
+  double2 *mine = xg + (((size_t)m * 2 + r) * 2 + g) * 2 * BR2XF_SLOT_D2;         // [slot][..]
+  const double2 *theirs = xg + (((size_t)m * 2 + (1 - r)) * 2 + g) * 2 * BR2XF_SLOT_D2;
+  constexpr size_t ROW = 4 * F::n;  // double2 per GGSW row
+  double2 ka[2][E], kb[2][E];
+  auto load_half = [&](double2 (&k)[2][E], const double2 *row, int o) {
+#pragma unroll
+    for (int l = 0; l < 2; ++l)
+#pragma unroll
+      for (int e = 0; e < E; ++e) k[l][e] = row[(o * 2 + l) * F::n + 4 * t + e];
+  };
+  uint32_t hc = 0;  // hand-offs so far (executed steps)
+#pragma unroll 1
+  for (int i = 0; i < NI; ++i) {
+    const int a = (int)__builtin_amdgcn_readfirstlane(lwe[i]) & (2 * NN - 1);
+    if (a == 0) continue;  // both workgroups of the message skip it
+    const size_t slot = hc & 1;
+    const double2 *rows = bskf + ((size_t)i * 2 * D2 + (size_t)r * D2 + (size_t)g * KD) * ROW;
+    load_half(ka, rows, 0);
+    uint32_t pk[2][E];  // digit word g of (X^a - 1) * ACC_r: digits 3g .. 3g + 2
+    {
+      int ts = t;
+      asm volatile("" : "+v"(ts));
+      const int j0 = F::idx(0, ts, 0), sb = F::slot_stage(j0);
+      if (g == 0) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int e = 0; e < E; ++e) ST[sb + F::idx(0, 0, e) + F::n * h] = ac[h][e];
+      }
+      wg_barrier_lds();
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const uint32_t u = (uint32_t)(j0 + F::idx(0, 0, e) + F::n * h - a) & (2 * NN - 1);
+          const double v = ST[F::slot_stage(u & (NN - 1))];
+          const uint32_t vh = (uint32_t)(__builtin_bit_cast(uint64_t, v) >> 32) ^ ((u & NN) << (31 - 11));
+          const double rot = __builtin_bit_cast(double, (__builtin_bit_cast(uint64_t, v) & 0xffffffffull) |
+                                                            ((uint64_t)vh << 32));
+          uint32_t w2[Digits2::DW];
+          Digits2::pack(canon_small<M>(rot - ST[sb + F::idx(0, 0, e) + F::n * h]), w2);
+          pk[h][e] = g ? w2[1] : w2[0];
+          asm volatile("" : "+v"(pk[h][e]));
+        }
+    }
+    double sr[2][2][E], si[2][2][E];  // [output][limb]
+#pragma unroll
+    for (int o = 0; o < 2; ++o)
+#pragma unroll
+      for (int l = 0; l < 2; ++l)
+#pragma unroll
+        for (int e = 0; e < E; ++e) sr[o][l][e] = si[o][l][e] = 0.0;
+    // digits on X0, X1, X0 (group 0's X1 held the staging, read before the first transform's barrier)
+#pragma unroll
+    for (int h = 0; h < KD; ++h) {
+      double xr[E], xi[E];
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        xr[e] = (double)((int)__builtin_amdgcn_ubfe(pk[0][e], 7 * h, h == 2 ? 8 : 7) - 64);
+        xi[e] = (double)((int)__builtin_amdgcn_ubfe(pk[1][e], 7 * h, h == 2 ? 8 : 7) - 64);
+      }
+      const double2 *row = rows + (size_t)h * ROW;
+      F::fwd(xr, xi, (h & 1) ? X1 : X0, W, tws, t);
+      load_half(kb, row, 1);
+#pragma unroll
+      for (int o = 0; o < 2; ++o) {
+#pragma unroll
+        for (int l = 0; l < 2; ++l)
+#pragma unroll
+          for (int e = 0; e < E; ++e) {
+            const double2 kv = o ? kb[l][e] : ka[l][e];
+            sr[o][l][e] = __fma_rn(xr[e], kv.x, __fma_rn(-xi[e], kv.y, sr[o][l][e]));
+            si[o][l][e] = __fma_rn(xr[e], kv.y, __fma_rn(xi[e], kv.x, si[o][l][e]));
+          }
+        if (o == 0 && h + 1 < KD) load_half(ka, row + ROW, 0);
+      }
+    }
+    // swap partials: group g keeps limb g of both outputs, sends limb 1 - g (both groups' X0, X1)
+    wg_barrier_lds();  // every transform's reads of X0 / X1 are done
+    {
+      double2 *to = buf[g ^ 1][0];  // the other group's X0, X1: [output][e * 256 + t]
+#pragma unroll
+      for (int o = 0; o < 2; ++o)
+#pragma unroll
+        for (int e = 0; e < E; ++e) to[o * F::n + e * F::T + t] = make_double2(sr[o][g ^ 1][e], si[o][g ^ 1][e]);
+    }
+    wg_barrier_lds();
+    double pr[2][E], pi[2][E];  // limb g of both outputs, this workgroup's six digits
+    {
+      const double2 *from = buf[g][0];
+#pragma unroll
+      for (int o = 0; o < 2; ++o)
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const double2 v = from[o * F::n + e * F::T + t];
+          pr[o][e] = (g ? sr[o][1][e] : sr[o][0][e]) + v.x;
+          pi[o][e] = (g ? si[o][1][e] : si[o][0][e]) + v.y;
+        }
+    }
+    // hand-off: output 1 - r to the partner CU, output r's partial back from it
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      double *d = reinterpret_cast<double *>(mine + slot * BR2XF_SLOT_D2 + e * F::T + t);
+      st_sc1(d, pr[1 - r][e]);
+      st_sc1(d + 1, pi[1 - r][e]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __hip_atomic_store(my_flag, hc + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      int n = 0;
+      while (__hip_atomic_load(their_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < hc + 1) {
+        if (++n == BR2X_SPIN) {
+          stop = 1;
+          atomicExch(err, 1);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+    }
+    __syncthreads();
+    if (stop) break;
+    double yr[E], yi[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const double *s2 = reinterpret_cast<const double *>(theirs + slot * BR2XF_SLOT_D2 + e * F::T + t);
+      yr[e] = pr[r][e] + ld_sc1(s2);
+      yi[e] = pi[r][e] + ld_sc1(s2 + 1);
+    }
+    // inverse of limb g (X0: the swap's reads of this group's X0 are done before the hand-off barrier)
+    F::inv(yr, yi, X0, W, tws, t);
+    // group 1: red(round(P_hi) 2^25) to group 0 through its X1; group 0: ACC_r += it + round(P_lo)
+    double *hx = reinterpret_cast<double *>(buf[1][1]);
+    if (g == 1) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        hx[e * F::T + t] = red<M>(rint(yr[e]) * LIMB);
+        hx[(E + e) * F::T + t] = red<M>(rint(yi[e]) * LIMB);
+      }
+    }
+    wg_barrier_lds();
+    if (g == 0) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        ac[0][e] = canon<M>(ac[0][e] + hx[e * F::T + t] + rint(yr[e]));
+        ac[1][e] = canon<M>(ac[1][e] + hx[(E + e) * F::T + t] + rint(yi[e]));
+      }
+    }
+    ++hc;
+  }
+  if (g == 0) {
+    uint64_t *o = out + (size_t)m * 2 * NN + (size_t)r * NN;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int e = 0; e < E; ++e) o[F::idx(0, t, e) + F::n * h] = to_u64<M>(ac[h][e]);
+  }
+}
+
 }  // namespace omr

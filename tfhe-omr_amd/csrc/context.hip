@@ -174,8 +174,9 @@ struct omr_ctx {
   // chunks of at most latency_max messages run the latency kernels (latency_kernels.hpp)
   size_t latency_max = OMR_DEFAULT_LATENCY_MAX;
   int *ks_part = nullptr;  // split key-switch partial sums, [KS_SPLIT][64][672][4]
-  // two-CU level-2 latency kernel (br2x_kernel, cooperative launch): partial hand-off slots
-  // [n][2][2][N2], flags [n][2], a timeout flag x_err that every launch copies to the pinned host
+  // two-CU level-2 latency kernel (br2xf_kernel on the FFT, or br2x_kernel in the OMR_LAT_NTT
+  // build; cooperative launch): partial hand-off slots (br2xf: [n][2][2 limbs][2][1024] double2,
+  // br2x: [n][2][2][N2] double), flags [n][2], a timeout flag x_err that every launch copies to the pinned host
   // word x_err_host on its stream (read by omr_ctx_check and at the start of the next call)
   double *x_slots = nullptr;
   uint32_t *x_flags = nullptr;
@@ -361,8 +362,8 @@ omr_status convert_keys_fft1(const uint32_t *host, size_t npoly, double2 *dev, c
 
 bool latency_path(const omr_ctx *c, size_t n) { return n <= c->latency_max; }
 
-// br2x_kernel's bounded hand-off wait: a workgroup whose partner never published leaves its loop
-// and sets x_err; each br2x launch then copies x_err to the pinned x_err_host on its stream. This
+// The two-CU kernel's bounded hand-off wait: a workgroup whose partner never published leaves its
+// loop and sets x_err; each launch then copies x_err to the pinned x_err_host on its stream. This
 // reports (and clears) an error whose copy has landed: callers sync the stream first for a
 // definitive answer (omr_ctx_check, the host entry points), or call it before enqueueing new work
 // (the device entry points) so a failed earlier call is never attributed to a later one.
@@ -405,19 +406,20 @@ omr_status launch_br1(omr_ctx *c, size_t n, const uint16_t *ca, const uint16_t *
   return OMR_OK;
 }
 
-// br2x_kernel over 2 n workgroups as a cooperative launch (co-residency guaranteed, or the launch
-// is refused); false when refused, so the caller falls back to br2l_kernel.
+// br2xf_kernel (br2x_kernel with -DOMR_LAT_NTT) over 2 n workgroups as a cooperative launch
+// (co-residency guaranteed, or the launch is refused); false when refused, so the caller falls
+// back to br2l_kernel.
 omr_status launch_br2x(omr_ctx *c, size_t n, const uint32_t *lwe_int, uint64_t *out, hipStream_t st,
                        bool *launched) {
   *launched = false;
-  if (!c->coop || 2 * n > (size_t)c->num_cu) return OMR_OK;  // one 150 KB-LDS workgroup per CU
+  if (!c->coop || 2 * n > (size_t)c->num_cu) return OMR_OK;  // one 112-150 KB-LDS workgroup per CU
   if (n > c->x_cap) {
     omr_status s;
     if ((s = scratch_idle(c)) != OMR_OK) return s;
     dev_free(c->x_slots);
     dev_free(c->x_flags);
     c->x_cap = 0;
-    HIP_TRY(hipMalloc(&c->x_slots, n * 4 * N2 * sizeof(double)));
+    HIP_TRY(hipMalloc(&c->x_slots, n * 8 * N2 * sizeof(double)));  // br2xf: [2][2 limbs][2][1024] double2
     HIP_TRY(hipMalloc(&c->x_flags, n * 2 * sizeof(uint32_t)));
     c->x_cap = n;
   }
@@ -433,15 +435,25 @@ omr_status launch_br2x(omr_ctx *c, size_t n, const uint32_t *lwe_int, uint64_t *
   double *slots = c->x_slots;
   uint32_t *flags = c->x_flags;
   int *err = c->x_err;
+#ifndef OMR_LAT_FFT  // the NTT two-CU kernel (br2xf_kernel on the FFT: -DOMR_LAT_FFT, slower)
   void *args[] = {(void *)&lwe_int, (void *)&bsk2, (void *)&tb, (void *)&slots, (void *)&flags, (void *)&err,
                   (void *)&out};
   const hipError_t e = hipLaunchCooperativeKernel(reinterpret_cast<const void *>(&br2x_kernel),
                                                   dim3((unsigned)(2 * n)), dim3(BR2L_T), args, 0, st);
+#else
+  (void)bsk2;
+  const double2 *bskf = c->bsk2f, *twg = c->fft2;
+  double2 *slots2 = reinterpret_cast<double2 *>(slots);
+  void *args[] = {(void *)&lwe_int, (void *)&bskf, (void *)&twg, (void *)&tb, (void *)&slots2, (void *)&flags,
+                  (void *)&err, (void *)&out};
+  const hipError_t e = hipLaunchCooperativeKernel(reinterpret_cast<const void *>(&br2xf_kernel),
+                                                  dim3((unsigned)(2 * n)), dim3(512), args, 0, st);
+#endif
   if (e == hipErrorCooperativeLaunchTooLarge || e == hipErrorNotSupported || e == hipErrorInvalidConfiguration) {
     (void)hipGetLastError();  // refused: nothing was enqueued
     return OMR_OK;
   }
-  if (e != hipSuccess) return set_error(OMR_ERR_DEVICE, std::string("br2x cooperative launch: ") + hipGetErrorString(e));
+  if (e != hipSuccess) return set_error(OMR_ERR_DEVICE, std::string("two-CU level-2 cooperative launch: ") + hipGetErrorString(e));
   HIP_TRY(hipMemcpyAsync(c->x_err_host, c->x_err, sizeof(int), hipMemcpyDeviceToHost, st));
   *launched = true;
   return OMR_OK;
