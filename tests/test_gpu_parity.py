@@ -167,9 +167,8 @@ def test_latency_level2_variants_match_throughput(real):
 
 
 def test_level2_throughput_small_batches(real):
-    """The throughput level-2 kernel (br2f_kernel; the -DOMR_L2_PAIR build's br2fp_kernel, two
-    messages per workgroup, has an odd tail here) at batches of 5 and 6 messages against the
-    latency kernels (oracle-checked NTT path), rotation and rotation + trace."""
+    """The throughput level-2 kernel (br2f_kernel, FFT) at batches of 5 and 6 messages against the
+    latency kernels (the oracle-checked NTT path), rotation and rotation + trace."""
     _, det, _ = real
     for n in (5, 6):
         mask = np.zeros(n, dtype=bool)

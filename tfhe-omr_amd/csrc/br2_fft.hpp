@@ -446,414 +446,4 @@ __global__ __launch_bounds__(256, 2) void br2f_kernel(const uint32_t *__restrict
   hom_trace_store(acc0, acc1, xch, tw, xch + 2 * NN, tk, tb, o, t);
 }
 
-
-// Level-2 blind rotation on the exact FFT, two messages per 512-thread workgroup (br2fp; build
-// variant -DOMR_L2_PAIR, not the production path): br2f_kernel streams 768 KB of FFT-domain key
-// per CMUX step and message from L2. Here the two 256-thread groups of a workgroup each transform
-// their own message's digits (group g, message g) and swap the spectra through LDS (S_g), so every
-// thread multiplies BOTH messages' spectra by the key blocks of ONE output (group g: output g, both
-// limbs): each key byte is read once per pair of messages, 384 KB per message-step. Group g owns
-// output g's accumulator of both messages, runs their four inverse transforms and recombines
-// them; the digits of message g are taken from accumulators staged in LDS by their owner. Same
-// rows, digits, transforms and rounding as br2f_kernel: bit-identical output. Measured 787 ms vs
-// 667 ms per 16,384 messages (profiles/r03/level2_experiments.log): the key stream is not what
-// binds br2f (an L1-resident key saves 12 %), and the extra workgroup-wide barrier per digit
-// across 8 waves costs more than the halved key traffic saves.
-//
-// Per digit: transform (X_g, one workgroup barrier; W_g wave-local), spectrum to S_g, barrier,
-// other spectrum from S_{1-g}, multiply-accumulate. A buffer is rewritten only after a barrier
-// that follows every read of it (the inverses alternate X_g and S_g).
-// LDS: twiddles 16 KB + (X, W, S) x 2 groups 96 KB + staging 32 KB = 144 KB, one workgroup per
-// CU (8 waves: two per SIMD, as two single-message workgroups).
-constexpr int BR2P_T = 512;
-__global__ __launch_bounds__(BR2P_T, 1) void br2fp_kernel(const uint32_t *__restrict__ lwe_int, size_t nmsg,
-                                                          const double2 *__restrict__ bskf,
-                                                          const double2 *__restrict__ twg, const double *__restrict__ tk,
-                                                          DeviceTables tb, uint64_t *__restrict__ out, int mode) {
-  using F = Fft1024;
-  using M = Mod<2>;
-  using DG = Digits2;
-  constexpr int E = F::E, NN = N2;
-  __shared__ double2 tws[F::n];
-  __shared__ double2 grp[2][3][F::n];      // per group: X, W, S
-  __shared__ double stage[2][NN];          // [message][coefficient] of one output poly
-  const int g = __builtin_amdgcn_readfirstlane(threadIdx.x >> 8), t = threadIdx.x & 255;
-  // staging slot of coefficient idx(0, t, e) + 1024 h: sb + idx(0, 0, e) + 1024 h (slot_stage only
-  // flips bit 4 by bit 6, both thread bits)
-  const int sb = F::slot_stage(F::idx(0, t, 0));
-  double2 *X = grp[g][0], *W = grp[g][1], *S = grp[g][2];
-  const double2 *So = grp[g ^ 1][2];
-  // messages of this workgroup: k = 0 "mine" (message g), k = 1 the other group's
-  const size_t m0 = 2 * (size_t)blockIdx.x;
-  const size_t mk[2] = {min(m0 + g, nmsg - 1), min(m0 + (g ^ 1), nmsg - 1)};
-  const uint32_t *lwe0 = lwe_int + min(m0, nmsg - 1) * (NI + 1);
-  const uint32_t *lwe1 = lwe_int + min(m0 + 1, nmsg - 1) * (NI + 1);
-  for (int j = threadIdx.x; j < F::TW_LEN; j += BR2P_T) tws[j] = twg[j];
-  // output g of message (g ^ k): ac[k][h][e] = coefficient idx(0, t, e) + 1024 h
-  double ac[2][2][E];
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const int b = (int)lwe_int[mk[k] * (NI + 1) + NI];
-    const int rr = (2 * NN - (b % (2 * NN))) % (2 * NN);
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int e = 0; e < E; ++e)
-        ac[k][h][e] = g == 0 ? 0.0 : canon_small<M>(rot_read<NN>(tb.lut2, F::idx(0, t, e) + F::n * h, rr));
-  }
-  __syncthreads();
-  double2 kv[2][E];  // this group's key blocks (output g, limbs 0 / 1) of the next digit in issue order
-  auto load_key = [&](const double2 *row) {
-#pragma unroll
-    for (int l = 0; l < 2; ++l)
-#pragma unroll
-      for (int e = 0; e < E; ++e) kv[l][e] = row[(g * 2 + l) * F::n + 4 * t + e];
-  };
-  constexpr size_t ROW = 4 * F::n;  // double2 per GGSW row
-#pragma unroll 1
-  for (int i = 0; i < NI; ++i) {
-    const int a0 = (int)__builtin_amdgcn_readfirstlane(lwe0[i]) & (2 * NN - 1);
-    const int a1 = (int)__builtin_amdgcn_readfirstlane(lwe1[i]) & (2 * NN - 1);
-    if ((a0 | a1) == 0) continue;  // (X^0 - 1) * ACC = 0 for both messages
-    const int a = g ? a1 : a0;     // wave-uniform
-    const double2 *step = bskf + (size_t)i * 2 * D2 * ROW;
-    load_key(step);
-    double sr[2][2][E], si[2][2][E];  // [message k][limb] spectra of output g
-#pragma unroll
-    for (int k = 0; k < 2; ++k)
-#pragma unroll
-      for (int l = 0; l < 2; ++l)
-#pragma unroll
-        for (int e = 0; e < E; ++e) sr[k][l][e] = si[k][l][e] = 0.0;
-#pragma unroll
-    for (int p = 0; p < 2; ++p) {
-      uint32_t pk[2][E][DG::DW];  // digit words of (X^a - 1) * ACC_p of message g
-      // the owner (group p) stages output p of both messages; group g reads message g's
-      if (g == p) {
-#pragma unroll
-        for (int k = 0; k < 2; ++k)
-#pragma unroll
-          for (int h = 0; h < 2; ++h)
-#pragma unroll
-            for (int e = 0; e < E; ++e) stage[g ^ k][sb + F::idx(0, 0, e) + F::n * h] = ac[k][h][e];
-      }
-      wg_barrier_lds();
-      {
-        const double *st = stage[g];
-#pragma unroll
-        for (int h = 0; h < 2; ++h)
-#pragma unroll
-          for (int e = 0; e < E; ++e) {
-            const int j = F::idx(0, t, e) + F::n * h;
-            const uint32_t u = (uint32_t)(j - a) & (2 * NN - 1);
-            const double v = st[F::slot_stage(u & (NN - 1))];
-            const uint32_t vh = (uint32_t)(__builtin_bit_cast(uint64_t, v) >> 32) ^ ((u & NN) << (31 - 11));
-            const double rot = __builtin_bit_cast(double, (__builtin_bit_cast(uint64_t, v) & 0xffffffffull) |
-                                                              ((uint64_t)vh << 32));
-            DG::pack(canon_small<M>(rot - st[sb + F::idx(0, 0, e) + F::n * h]), pk[h][e]);
-            asm volatile("" : "+v"(pk[h][e][0]), "+v"(pk[h][e][1]));
-          }
-      }
-      // digits in issue order g' = 2 j + w (digit j + 3 w: word w, field j; GGSW row p D2 + j + 3 w)
-#pragma unroll 1
-      for (int j = 0; j < D2 / 2; ++j) {
-#pragma unroll
-        for (int w = 0; w < 2; ++w) {
-          double xr[E], xi[E];
-#pragma unroll
-          for (int e = 0; e < E; ++e) {
-            xr[e] = (double)((int)__builtin_amdgcn_ubfe(pk[0][e][w], 7 * j, j == 2 ? 8 : 7) - 64);
-            xi[e] = (double)((int)__builtin_amdgcn_ubfe(pk[1][e][w], 7 * j, j == 2 ? 8 : 7) - 64);
-          }
-          const int nx = w == 0 ? p * D2 + j + 3 : (j + 1 < D2 / 2 ? p * D2 + j + 1 : (p == 0 ? D2 : 2 * D2 - 1));
-          const double2 *next = step + (size_t)nx * ROW;
-          F::fwd(xr, xi, X, W, tws, t);
-#pragma unroll
-          for (int e = 0; e < E; ++e) S[e * F::T + t] = make_double2(xr[e], xi[e]);
-          wg_barrier_lds();
-          double yr[E], yi[E];
-#pragma unroll
-          for (int e = 0; e < E; ++e) {
-            const double2 v = So[e * F::T + t];
-            yr[e] = v.x;
-            yi[e] = v.y;
-          }
-#pragma unroll
-          for (int l = 0; l < 2; ++l)
-#pragma unroll
-            for (int e = 0; e < E; ++e) {
-              const double2 k = kv[l][e];
-              sr[0][l][e] = __fma_rn(xr[e], k.x, __fma_rn(-xi[e], k.y, sr[0][l][e]));
-              si[0][l][e] = __fma_rn(xr[e], k.y, __fma_rn(xi[e], k.x, si[0][l][e]));
-              sr[1][l][e] = __fma_rn(yr[e], k.x, __fma_rn(-yi[e], k.y, sr[1][l][e]));
-              si[1][l][e] = __fma_rn(yr[e], k.y, __fma_rn(yi[e], k.x, si[1][l][e]));
-            }
-          load_key(next);  // the last digit reloads its own row: harmless
-        }
-      }
-    }
-    // inverses (X, S, X, S), rounding to the exact limb products, recombination mod q2
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-#pragma unroll
-      for (int l = 0; l < 2; ++l) F::inv(sr[k][l], si[k][l], l ? S : X, W, tws, t);
-#pragma unroll
-      for (int e = 0; e < E; ++e)
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const double lo = rint(h ? si[k][0][e] : sr[k][0][e]);
-          const double hi = rint(h ? si[k][1][e] : sr[k][1][e]) * LIMB;
-          ac[k][h][e] = canon<M>(ac[k][h][e] + red<M>(hi) + lo);
-        }
-    }
-  }
-  if (mode == 1) {
-    // group g stores output g of both messages (each message's owner pair covers both outputs)
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      if (m0 + (g ^ k) >= nmsg) continue;
-      uint64_t *o = out + (m0 + (g ^ k)) * 2 * NN + g * NN;
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int e = 0; e < E; ++e) o[F::idx(0, t, e) + F::n * h] = to_u64<M>(ac[k][h][e]);
-    }
-    return;
-  }
-  // hom_trace per group on its own message: mask / body of message g in the trace layout
-  double *xfer = reinterpret_cast<double *>(&grp[0][0][0]);  // [message][output][N2] doubles, 64 KB
-  __syncthreads();  // the last inverses' reads are done everywhere
-#pragma unroll
-  for (int k = 0; k < 2; ++k)
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int e = 0; e < E; ++e) xfer[((g ^ k) * 2 + g) * NN + F::idx(0, t, e) + F::n * h] = ac[k][h][e];
-  __syncthreads();
-  double acc0[BR2_E], acc1[BR2_E];
-#pragma unroll
-  for (int e = 0; e < BR2_E; ++e) {
-    acc0[e] = xfer[(g * 2 + 0) * NN + t + e * BR2_T];
-    acc1[e] = xfer[(g * 2 + 1) * NN + t + e * BR2_T];
-  }
-  __syncthreads();
-  double *tw = reinterpret_cast<double *>(tws);  // N2 doubles
-  double *itw = &stage[0][0];                     // N2 doubles
-  for (int j = threadIdx.x; j < NN; j += BR2P_T) {
-    tw[j] = tb.tw2[j];
-    itw[j] = tb.itw2[j];
-  }
-  __syncthreads();
-  double *xch = reinterpret_cast<double *>(&grp[g][0][0]);  // 2 N2 doubles (X, W) per group
-  // (an odd tail's group 1 repeats the last message and stores the same values as group 0)
-  hom_trace_store(acc0, acc1, xch, tw, itw, tk, tb, out + mk[0] * 2 * NN, t);
-}
-
-
-// ---- level-2 latency on the exact FFT, two CUs per message (br2xf) ---------------------------
-// The latency path's level 2 (br2x_kernel's protocol, latency_kernels.hpp) with br2f's transform:
-// workgroup 2m + r (512 threads, one per CU) owns polynomial r of message m (0 mask, 1 body) and its
-// accumulator (group 0). Per CMUX step: group 0 stages ACC_r; group g decomposes it and transforms
-// digits 3g .. 3g + 2 (one digit word per coefficient), multiply-accumulating all four (output,
-// limb) spectra with GGSW rows r D2 + 3g + h; the groups swap partials so that group g holds limb
-// g of both outputs summed over the workgroup's six digits; group g hands its output-(1 - r)
-// partial of limb g to the partner CU through global memory (sc1 stores, flag hc + 1 per executed
-// step, slot hc & 1, bounded poll: br2x's hand-off rules) and adds the partner's output-r partial;
-// group g runs the inverse of limb g (the two limbs in parallel), group 1 passes its rounded,
-// 2^25-scaled limb to group 0 through LDS and group 0 updates ACC_r. Per step and group: three
-// forward FFTs and one inverse instead of br2x's three forward NTTs and (group 0) one inverse.
-// Same digits, rows and exact rounding as br2f_kernel: bit-identical. LDS: twiddles 16 KB + per
-// group X0, X1, W (96 KB); the staging (group 0's X1), the partial swap (both groups' X0, X1) and
-// the limb hand-over (group 1's X1) alias them between barriers.
-// Global slots: xg[m][r][limb][slot][e * 256 + t] double2 (16 KB per limb and slot).
-constexpr size_t BR2XF_SLOT_D2 = 1024;  // double2 per hand-off slot: one limb spectrum (4 points x 256 threads)
-__global__ __launch_bounds__(512, 1) void br2xf_kernel(const uint32_t *__restrict__ lwe_int,
-                                                       const double2 *__restrict__ bskf,
-                                                       const double2 *__restrict__ twg, DeviceTables tb,
-                                                       double2 *xg, uint32_t *flags, int *err,
-                                                       uint64_t *__restrict__ out) {
-  using F = Fft1024;
-  using M = Mod<2>;
-  constexpr int E = F::E, NN = N2, KD = D2 / 2;
-  __shared__ double2 tws[F::n];
-  __shared__ double2 buf[2][3][F::n];  // per group: X0, X1, W
-  __shared__ int stop;
-  const int m = blockIdx.x >> 1, r = blockIdx.x & 1;
-  const int g = __builtin_amdgcn_readfirstlane(threadIdx.x >> 8), t = threadIdx.x & 255;
-  double2 *X0 = buf[g][0], *X1 = buf[g][1], *W = buf[g][2];
-  double *ST = reinterpret_cast<double *>(buf[0][1]);  // staged ACC_r (group 0's X1)
-  const uint32_t *lwe = lwe_int + (size_t)m * (NI + 1);
-  for (int j = threadIdx.x; j < F::TW_LEN; j += 512) tws[j] = twg[j];
-  double ac[2][E];  // ACC_r, group 0: coefficient idx(0, t, e) + 1024 h
-  {
-    const int b = (int)lwe[NI];
-    const int rr = (2 * NN - (b % (2 * NN))) % (2 * NN);
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int e = 0; e < E; ++e)
-        ac[h][e] = r == 1 ? canon_small<M>(rot_read<NN>(tb.lut2, F::idx(0, t, e) + F::n * h, rr)) : 0.0;
-  }
-  if (threadIdx.x == 0) stop = 0;
-  __syncthreads();
-  uint32_t *my_flag = flags + 2 * m + r, *their_flag = flags + 2 * m + (1 - r);
-  double2 *mine = xg + (((size_t)m * 2 + r) * 2 + g) * 2 * BR2XF_SLOT_D2;         // [slot][..]
-  const double2 *theirs = xg + (((size_t)m * 2 + (1 - r)) * 2 + g) * 2 * BR2XF_SLOT_D2;
-  constexpr size_t ROW = 4 * F::n;  // double2 per GGSW row
-  double2 ka[2][E], kb[2][E];
-  auto load_half = [&](double2 (&k)[2][E], const double2 *row, int o) {
-#pragma unroll
-    for (int l = 0; l < 2; ++l)
-#pragma unroll
-      for (int e = 0; e < E; ++e) k[l][e] = row[(o * 2 + l) * F::n + 4 * t + e];
-  };
-  uint32_t hc = 0;  // hand-offs so far (executed steps)
-#pragma unroll 1
-  for (int i = 0; i < NI; ++i) {
-    const int a = (int)__builtin_amdgcn_readfirstlane(lwe[i]) & (2 * NN - 1);
-    if (a == 0) continue;  // both workgroups of the message skip it
-    const size_t slot = hc & 1;
-    const double2 *rows = bskf + ((size_t)i * 2 * D2 + (size_t)r * D2 + (size_t)g * KD) * ROW;
-    load_half(ka, rows, 0);
-    uint32_t pk[2][E];  // digit word g of (X^a - 1) * ACC_r: digits 3g .. 3g + 2
-    {
-      int ts = t;
-      asm volatile("" : "+v"(ts));
-      const int j0 = F::idx(0, ts, 0), sb = F::slot_stage(j0);
-      if (g == 0) {
-#pragma unroll
-        for (int h = 0; h < 2; ++h)
-#pragma unroll
-          for (int e = 0; e < E; ++e) ST[sb + F::idx(0, 0, e) + F::n * h] = ac[h][e];
-      }
-      wg_barrier_lds();
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int e = 0; e < E; ++e) {
-          const uint32_t u = (uint32_t)(j0 + F::idx(0, 0, e) + F::n * h - a) & (2 * NN - 1);
-          const double v = ST[F::slot_stage(u & (NN - 1))];
-          const uint32_t vh = (uint32_t)(__builtin_bit_cast(uint64_t, v) >> 32) ^ ((u & NN) << (31 - 11));
-          const double rot = __builtin_bit_cast(double, (__builtin_bit_cast(uint64_t, v) & 0xffffffffull) |
-                                                            ((uint64_t)vh << 32));
-          uint32_t w2[Digits2::DW];
-          Digits2::pack(canon_small<M>(rot - ST[sb + F::idx(0, 0, e) + F::n * h]), w2);
-          pk[h][e] = g ? w2[1] : w2[0];
-          asm volatile("" : "+v"(pk[h][e]));
-        }
-    }
-    double sr[2][2][E], si[2][2][E];  // [output][limb]
-#pragma unroll
-    for (int o = 0; o < 2; ++o)
-#pragma unroll
-      for (int l = 0; l < 2; ++l)
-#pragma unroll
-        for (int e = 0; e < E; ++e) sr[o][l][e] = si[o][l][e] = 0.0;
-    // digits on X0, X1, X0 (group 0's X1 held the staging, read before the first transform's barrier)
-#pragma unroll
-    for (int h = 0; h < KD; ++h) {
-      double xr[E], xi[E];
-#pragma unroll
-      for (int e = 0; e < E; ++e) {
-        xr[e] = (double)((int)__builtin_amdgcn_ubfe(pk[0][e], 7 * h, h == 2 ? 8 : 7) - 64);
-        xi[e] = (double)((int)__builtin_amdgcn_ubfe(pk[1][e], 7 * h, h == 2 ? 8 : 7) - 64);
-      }
-      const double2 *row = rows + (size_t)h * ROW;
-      F::fwd(xr, xi, (h & 1) ? X1 : X0, W, tws, t);
-      load_half(kb, row, 1);
-#pragma unroll
-      for (int o = 0; o < 2; ++o) {
-#pragma unroll
-        for (int l = 0; l < 2; ++l)
-#pragma unroll
-          for (int e = 0; e < E; ++e) {
-            const double2 kv = o ? kb[l][e] : ka[l][e];
-            sr[o][l][e] = __fma_rn(xr[e], kv.x, __fma_rn(-xi[e], kv.y, sr[o][l][e]));
-            si[o][l][e] = __fma_rn(xr[e], kv.y, __fma_rn(xi[e], kv.x, si[o][l][e]));
-          }
-        if (o == 0 && h + 1 < KD) load_half(ka, row + ROW, 0);
-      }
-    }
-    // swap partials: group g keeps limb g of both outputs, sends limb 1 - g (both groups' X0, X1)
-    wg_barrier_lds();  // every transform's reads of X0 / X1 are done
-    {
-      double2 *to = buf[g ^ 1][0];  // the other group's X0, X1: [output][e * 256 + t]
-#pragma unroll
-      for (int o = 0; o < 2; ++o)
-#pragma unroll
-        for (int e = 0; e < E; ++e) to[o * F::n + e * F::T + t] = make_double2(sr[o][g ^ 1][e], si[o][g ^ 1][e]);
-    }
-    wg_barrier_lds();
-    double pr[2][E], pi[2][E];  // limb g of both outputs, this workgroup's six digits
-    {
-      const double2 *from = buf[g][0];
-#pragma unroll
-      for (int o = 0; o < 2; ++o)
-#pragma unroll
-        for (int e = 0; e < E; ++e) {
-          const double2 v = from[o * F::n + e * F::T + t];
-          pr[o][e] = (g ? sr[o][1][e] : sr[o][0][e]) + v.x;
-          pi[o][e] = (g ? si[o][1][e] : si[o][0][e]) + v.y;
-        }
-    }
-    // hand-off: output 1 - r to the partner CU, output r's partial back from it
-#pragma unroll
-    for (int e = 0; e < E; ++e) {
-      double *d = reinterpret_cast<double *>(mine + slot * BR2XF_SLOT_D2 + e * F::T + t);
-      st_sc1(d, pr[1 - r][e]);
-      st_sc1(d + 1, pi[1 - r][e]);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      __hip_atomic_store(my_flag, hc + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      int n = 0;
-      while (__hip_atomic_load(their_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < hc + 1) {
-        if (++n == BR2X_SPIN) {
-          stop = 1;
-          atomicExch(err, 1);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(2);
-      }
-    }
-    __syncthreads();
-    if (stop) break;
-    double yr[E], yi[E];
-#pragma unroll
-    for (int e = 0; e < E; ++e) {
-      const double *s2 = reinterpret_cast<const double *>(theirs + slot * BR2XF_SLOT_D2 + e * F::T + t);
-      yr[e] = pr[r][e] + ld_sc1(s2);
-      yi[e] = pi[r][e] + ld_sc1(s2 + 1);
-    }
-    // inverse of limb g (X0: the swap's reads of this group's X0 are done before the hand-off barrier)
-    F::inv(yr, yi, X0, W, tws, t);
-    // group 1: red(round(P_hi) 2^25) to group 0 through its X1; group 0: ACC_r += it + round(P_lo)
-    double *hx = reinterpret_cast<double *>(buf[1][1]);
-    if (g == 1) {
-#pragma unroll
-      for (int e = 0; e < E; ++e) {
-        hx[e * F::T + t] = red<M>(rint(yr[e]) * LIMB);
-        hx[(E + e) * F::T + t] = red<M>(rint(yi[e]) * LIMB);
-      }
-    }
-    wg_barrier_lds();
-    if (g == 0) {
-#pragma unroll
-      for (int e = 0; e < E; ++e) {
-        ac[0][e] = canon<M>(ac[0][e] + hx[e * F::T + t] + rint(yr[e]));
-        ac[1][e] = canon<M>(ac[1][e] + hx[(E + e) * F::T + t] + rint(yi[e]));
-      }
-    }
-    ++hc;
-  }
-  if (g == 0) {
-    uint64_t *o = out + (size_t)m * 2 * NN + (size_t)r * NN;
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int e = 0; e < E; ++e) o[F::idx(0, t, e) + F::n * h] = to_u64<M>(ac[h][e]);
-  }
-}
-
 }  // namespace omr

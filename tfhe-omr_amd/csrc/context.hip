@@ -174,9 +174,8 @@ struct omr_ctx {
   // chunks of at most latency_max messages run the latency kernels (latency_kernels.hpp)
   size_t latency_max = OMR_DEFAULT_LATENCY_MAX;
   int *ks_part = nullptr;  // split key-switch partial sums, [KS_SPLIT][64][672][4]
-  // two-CU level-2 latency kernel (br2xf_kernel on the FFT, or br2x_kernel in the OMR_LAT_NTT
-  // build; cooperative launch): partial hand-off slots (br2xf: [n][2][2 limbs][2][1024] double2,
-  // br2x: [n][2][2][N2] double), flags [n][2], a timeout flag x_err that every launch copies to the pinned host
+  // two-CU level-2 latency kernel (br2x_kernel, cooperative launch): partial hand-off slots
+  // [n][2][2][N2], flags [n][2], a timeout flag x_err that every launch copies to the pinned host
   // word x_err_host on its stream (read by omr_ctx_check and at the start of the next call)
   double *x_slots = nullptr;
   uint32_t *x_flags = nullptr;
@@ -210,13 +209,7 @@ struct omr_ctx {
 
 #define OMR_BR1_NAME "br1f_kernel"
 #define OMR_KS_NAME "ks_mfma_kernel"
-#ifdef OMR_L2_NTT  // build variant: level 2 on the modular NTT (round-2 kernel), for A/B runs
-#define OMR_BR2_NAME "br2_trace_kernel"
-#elif defined(OMR_L2_PAIR)  // build variant: two messages per workgroup (br2fp_kernel)
-#define OMR_BR2_NAME "br2fp_kernel"
-#else
 #define OMR_BR2_NAME "br2f_kernel"
-#endif
 
 namespace {
 
@@ -406,20 +399,19 @@ omr_status launch_br1(omr_ctx *c, size_t n, const uint16_t *ca, const uint16_t *
   return OMR_OK;
 }
 
-// br2xf_kernel (br2x_kernel with -DOMR_LAT_NTT) over 2 n workgroups as a cooperative launch
-// (co-residency guaranteed, or the launch is refused); false when refused, so the caller falls
-// back to br2l_kernel.
+// br2x_kernel over 2 n workgroups as a cooperative launch (co-residency guaranteed, or the launch
+// is refused); false when refused, so the caller falls back to br2l_kernel.
 omr_status launch_br2x(omr_ctx *c, size_t n, const uint32_t *lwe_int, uint64_t *out, hipStream_t st,
                        bool *launched) {
   *launched = false;
-  if (!c->coop || 2 * n > (size_t)c->num_cu) return OMR_OK;  // one 112-150 KB-LDS workgroup per CU
+  if (!c->coop || 2 * n > (size_t)c->num_cu) return OMR_OK;  // one 150 KB-LDS workgroup per CU
   if (n > c->x_cap) {
     omr_status s;
     if ((s = scratch_idle(c)) != OMR_OK) return s;
     dev_free(c->x_slots);
     dev_free(c->x_flags);
     c->x_cap = 0;
-    HIP_TRY(hipMalloc(&c->x_slots, n * 8 * N2 * sizeof(double)));  // br2xf: [2][2 limbs][2][1024] double2
+    HIP_TRY(hipMalloc(&c->x_slots, n * 4 * N2 * sizeof(double)));
     HIP_TRY(hipMalloc(&c->x_flags, n * 2 * sizeof(uint32_t)));
     c->x_cap = n;
   }
@@ -435,25 +427,15 @@ omr_status launch_br2x(omr_ctx *c, size_t n, const uint32_t *lwe_int, uint64_t *
   double *slots = c->x_slots;
   uint32_t *flags = c->x_flags;
   int *err = c->x_err;
-#ifndef OMR_LAT_FFT  // the NTT two-CU kernel (br2xf_kernel on the FFT: -DOMR_LAT_FFT, slower)
   void *args[] = {(void *)&lwe_int, (void *)&bsk2, (void *)&tb, (void *)&slots, (void *)&flags, (void *)&err,
                   (void *)&out};
   const hipError_t e = hipLaunchCooperativeKernel(reinterpret_cast<const void *>(&br2x_kernel),
                                                   dim3((unsigned)(2 * n)), dim3(BR2L_T), args, 0, st);
-#else
-  (void)bsk2;
-  const double2 *bskf = c->bsk2f, *twg = c->fft2;
-  double2 *slots2 = reinterpret_cast<double2 *>(slots);
-  void *args[] = {(void *)&lwe_int, (void *)&bskf, (void *)&twg, (void *)&tb, (void *)&slots2, (void *)&flags,
-                  (void *)&err, (void *)&out};
-  const hipError_t e = hipLaunchCooperativeKernel(reinterpret_cast<const void *>(&br2xf_kernel),
-                                                  dim3((unsigned)(2 * n)), dim3(512), args, 0, st);
-#endif
   if (e == hipErrorCooperativeLaunchTooLarge || e == hipErrorNotSupported || e == hipErrorInvalidConfiguration) {
     (void)hipGetLastError();  // refused: nothing was enqueued
     return OMR_OK;
   }
-  if (e != hipSuccess) return set_error(OMR_ERR_DEVICE, std::string("two-CU level-2 cooperative launch: ") + hipGetErrorString(e));
+  if (e != hipSuccess) return set_error(OMR_ERR_DEVICE, std::string("br2x cooperative launch: ") + hipGetErrorString(e));
   HIP_TRY(hipMemcpyAsync(c->x_err_host, c->x_err, sizeof(int), hipMemcpyDeviceToHost, st));
   *launched = true;
   return OMR_OK;
@@ -471,19 +453,8 @@ omr_status launch_br2(omr_ctx *c, size_t n, const uint32_t *lwe_int, uint64_t *o
     if (!two_cu) br2l_kernel<<<(unsigned)n, BR2L_T, 0, st>>>(lwe_int, c->bsk2, c->tb, out);
     split_trace = true;
   } else {
-#ifdef OMR_L2_NTT
-    if (split_trace && mode == 0) {
-      br2_trace_kernel<<<(unsigned)n, BR2_T, 0, st>>>(lwe_int, c->bsk2, c->tk, c->tb, out, 1);
-    } else {
-      br2_trace_kernel<<<(unsigned)n, BR2_T, 0, st>>>(lwe_int, c->bsk2, c->tk, c->tb, out, mode);
-    }
-#elif defined(OMR_L2_PAIR)
-    br2fp_kernel<<<(unsigned)((n + 1) / 2), BR2P_T, 0, st>>>(lwe_int, n, c->bsk2f, c->fft2, c->tk, c->tb, out,
-                                                             split_trace && mode == 0 ? 1 : mode);
-#else
     br2f_kernel<<<(unsigned)n, Fft1024::T, 0, st>>>(lwe_int, c->bsk2f, c->fft2, c->tk, c->tb, out,
                                                     split_trace && mode == 0 ? 1 : mode);
-#endif
   }
   HIP_TRY(hipGetLastError());
   if (mid) HIP_TRY(hipEventRecord(mid, st));

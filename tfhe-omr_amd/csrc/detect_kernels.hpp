@@ -108,96 +108,6 @@ struct KeyRow {
   }
 };
 
-// One CMUX step of the level-2 binary blind rotation (BlindRotationKey::blind_rotate):
-//   ACC += ((X^a - 1) * ACC) [x] GGSW_i
-// acc0/acc1: mask / body accumulator, coefficient tid + e*T, canonical, in registers. ggsw: the
-// NTT-domain rows [2D][2][N] in the CmuxNtt output order, pre-scaled by N^-1. Three-buffer
-// exchanges (xch holds CmuxNtt::LDS_DOUBLES), tw the permuted table tw2c.
-// Cross-wave uses of the LDS per step, in order: staging of the mask in X1, the 6 mask-digit
-// NTTs on X0, X1, X0, X1, X0, X1, staging of the body in X0, the 6 body-digit NTTs on X1, X0,
-// ..., X0, the inverse A on X1 and B on X0; the step starts on X1 and ends on X0. Consecutive
-// cross-wave uses always alternate, so each writes a buffer whose last readers have passed the
-// other buffer's barrier: no transform and no staging needs a trailing barrier, 16 workgroup
-// barriers per step (one per cross-wave use) instead of 32.
-template <int T, int E, typename KeyT>
-__device__ __forceinline__ void cmux_step3(double (&acc0)[E], double (&acc1)[E], double *xch, int a,
-                                           const KeyT *__restrict__ ggsw, const double *tw, int tid,
-                                           const double *t0, const double *__restrict__ gtw) {
-  using M = Mod<2>;
-  using NTT = CmuxNtt;
-  using DG = Digits2;
-  constexpr int N = M::N;
-  static_assert(T == NTT::T && E == NTT::E, "CMUX transform geometry");
-  static_assert(D2 % 2 == 0, "digit loop unrolled by two (alternating cross-wave buffers)");
-  double accA[E], accB[E];
-#pragma unroll
-  for (int e = 0; e < E; ++e) accA[e] = accB[e] = 0.0;
-  KeyRow<KeyT, E> cur;
-  cur.load(ggsw, N, tid * E);
-  uint32_t pk[E][DG::DW];
-#pragma unroll
-  for (int p = 0; p < 2; ++p) {
-    {  // digits of (X^a - 1) * ACC_p, staged in X1 (mask) / X0 (body)
-      double *st = xch + (p == 0 ? N : 0);
-#pragma unroll
-      for (int e = 0; e < E; ++e) st[tid + e * T] = p == 0 ? acc0[e] : acc1[e];
-      __syncthreads();
-#pragma unroll
-      for (int e = 0; e < E; ++e)
-        DG::pack(canon_small<M>(rot_read_lds<N>(st, tid + e * T, a) - (p == 0 ? acc0[e] : acc1[e])), pk[e]);
-      __builtin_amdgcn_wave_barrier();
-      __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    }
-    // digit pairs (j, j + 3): the pair's two digits sit at the same offset of words 0 and 1.
-    // Products are counted in issue order g (reductions every fourth, as before; the sum is exact
-    // in any order), and the key row of the next digit in that order is loaded one digit ahead.
-#pragma unroll 1
-    for (int j = 0; j < D2 / 2; ++j) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int g = p * D2 + 2 * j + h;  // issue order
-        int f[E];
-#pragma unroll
-        for (int e = 0; e < E; ++e) f[e] = h == 0 ? DG::template field<0>(pk[e], j) : DG::template field<1>(pk[e], j);
-        double x[E];
-        if ((h ^ p) == 0)  // mask digits on X0, X1, ...; body digits on X1, X0, ...
-          NTT::template fwd_small<0>(f, t0, x, xch, tw, tid, gtw);
-        else
-          NTT::template fwd_small<1>(f, t0, x, xch, tw, tid, gtw);
-#pragma unroll
-        for (int e = 0; e < E; ++e) {
-          accA[e] += mm<M>(x[e], (double)cur.a[e]);
-          accB[e] += mm<M>(x[e], (double)cur.b[e]);
-        }
-        // |x| <= 6.72q after the transform, so |mm(x, key)| <= 1.76q: four products on a
-        // reduced sum stay below 7.6q < 8q < 2^53 (tests/test_fp64_residues.py)
-        if ((g % 4) == 3 && g + 1 < 2 * D2) {
-#pragma unroll
-          for (int e = 0; e < E; ++e) {
-            accA[e] = red<M>(accA[e]);
-            accB[e] = red<M>(accB[e]);
-          }
-        }
-        if (g + 1 < 2 * D2) {  // row of the next digit: (j, h = 1), (j + 1, h = 0) or the body's first
-          const int nr = h == 0 ? p * D2 + j + 3 : (j + 1 < D2 / 2 ? p * D2 + j + 1 : (p + 1) * D2);
-          cur.load(ggsw + (size_t)nr * 2 * N, N, tid * E);
-        }
-      }
-    }
-  }
-#pragma unroll
-  for (int e = 0; e < E; ++e) {
-    accA[e] = red<M>(accA[e]);
-    accB[e] = red<M>(accB[e]);
-  }
-  NTT::inv2(accA, accB, xch, tw, tid, gtw);  // A through X1, then B through X0
-#pragma unroll
-  for (int e = 0; e < E; ++e) {
-    acc0[e] = canon<M>(acc0[e] + accA[e]);
-    acc1[e] = canon<M>(acc1[e] + accB[e]);
-  }
-}
-
 // Sum of the 7 extracted LWEs mod q1 (detector.rs:556), transposed to [N1+1][B] for the key
 // switch (lanes = messages).
 __global__ void sum7_kernel(const uint32_t *__restrict__ ext, uint32_t *__restrict__ lwe1t,
@@ -306,71 +216,6 @@ __device__ __forceinline__ void hom_trace_store(double (&acc0)[BR2_E], double (&
     o[t] = to_u64<M>(canon<M>(ca[e]));
     o[N + t] = to_u64<M>(cb[e]);
   }
-}
-
-// ------------------------------------------------------------------------------------------
-// Level 2 (second_level_bootstrapping, detector.rs:599-624) fused with hom_trace (:626-639):
-// one workgroup per message. mode 0: trace + NTT output u64 [wg][2][N2] (NttRlweCiphertext);
-// mode 1: blind rotation only, coefficient-domain output (stage test).
-// ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(BR2_T, BR2_WAVES) void br2_trace_kernel(const uint32_t *__restrict__ lwe_int,
-                                                         const double *__restrict__ bsk2,
-                                                         const double *__restrict__ tk,
-                                                         DeviceTables tb,
-                                                         uint64_t *__restrict__ out, int mode) {
-  using M = Mod<2>;
-  constexpr int T = BR2_T, E = BR2_E, N = N2;
-  using NTT = WgNtt<M, T, E>;
-  __shared__ double xch[NTT::LDS3_DOUBLES];
-  // forward twiddles (the inverse reads them mirrored) + the five small-digit stage tables
-  __shared__ double tws[N + 136 * 5];
-  const int tid = threadIdx.x;
-  const size_t wg = blockIdx.x;
-  const uint32_t *lwe = lwe_int + wg * (NI + 1);
-  double acc0[E], acc1[E];
-  const double *tw = tws, *t0 = tws + N;
-  {  // ACC = (0, X^{-b} * LUT2)
-    const int b = (int)lwe[NI];
-    const int rr = (2 * N - (b % (2 * N))) % (2 * N);
-#pragma unroll
-    for (int e = 0; e < E; ++e) {
-      const int j = tid + e * T;
-      acc0[e] = 0.0;
-      acc1[e] = canon_small<M>(rot_read<N>(tb.lut2, j, rr));
-      tws[j] = tb.tw2c[j];  // CMUX transforms: stages 9, 10 permuted (CmuxNtt)
-    }
-    if (tid <= 128) {  // table k: d * c_k, d = tid - 64 (c = tw1, tw2, tw1 tw2, tw3, tw1 tw3)
-      const double w1 = tb.tw2[1], w2 = tb.tw2[2], w3 = tb.tw2[3];
-      const double c[5] = {w1, w2, canon<M>(mm<M>(w1, w2)), w3, canon<M>(mm<M>(w1, w3))};
-#pragma unroll
-      for (int k = 0; k < 5; ++k) tws[N + 136 * k + tid] = canon<M>(mm<M>((double)(tid - 64), c[k]));
-    }
-    __syncthreads();
-  }
-#pragma unroll 1
-  for (int i = 0; i < NI; ++i) {
-    const int a = (int)__builtin_amdgcn_readfirstlane(lwe[i]) & (2 * N - 1);
-    if (a == 0) continue;  // (X^0 - 1) * ACC = 0
-    cmux_step3<T, E, double>(acc0, acc1, xch, a, bsk2 + (size_t)i * (2 * D2 * 2 * N), tw, tid, t0, tb.tw2c);
-  }
-  uint64_t *o = out + wg * 2 * N;
-  if (mode == 1) {
-#pragma unroll
-    for (int e = 0; e < E; ++e) {
-      o[tid + e * T] = to_u64<M>(acc0[e]);
-      o[N + tid + e * T] = to_u64<M>(acc1[e]);
-    }
-    return;
-  }
-  __syncthreads();  // the last inverse's cross-wave reads of X0 are done everywhere
-  double *itw_t = xch + 2 * N;  // the trace's inverse table goes to the W buffer
-#pragma unroll
-  for (int e = 0; e < E; ++e) {
-    itw_t[tid + e * T] = tb.itw2[tid + e * T];
-    tws[tid + e * T] = tb.tw2[tid + e * T];  // the trace's (generic) transforms read tw2
-  }
-  __syncthreads();
-  hom_trace_store(acc0, acc1, xch, tw, itw_t, tk, tb, o, tid);
 }
 
 }  // namespace omr

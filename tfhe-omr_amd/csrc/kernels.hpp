@@ -7,12 +7,11 @@
 namespace omr {
 
 // Workgroup geometry per level (T threads x E residues per thread = N) of the modular NTTs.
-// Level 2 (blind rotation, trace, encode, key conversion): 256 threads x 8 residues, 2 waves/SIMD.
-// Level 1 only needs the NTT for omr_ntt (tests); its blind rotation runs on the complex FFT
-// (br1_fft.hpp).
+// Level 2 (latency blind rotations, trace, encode, key conversion): 256 threads x 8 residues.
+// Both throughput blind rotations run on exact complex FFTs (br1_fft.hpp, br2_fft.hpp); level 1
+// needs the NTT only for omr_ntt (tests).
 constexpr int BR1_T = 256, BR1_E = 4;  // N1 = 1024
 constexpr int BR2_T = 256, BR2_E = 8;  // N2 = 2048
-constexpr int BR2_WAVES = 2;
 constexpr int ENC_T = 128, ENC_E = 16;
 constexpr size_t OMR_DEFAULT_BATCH = 16384;  // messages per detect chunk (scratch 36 KiB/msg)
 constexpr size_t OMR_ENC_MAX_CHUNKS = 4096;   // default chunk partials per encode ciphertext

@@ -166,7 +166,7 @@ __global__ __launch_bounds__(64 * BR1L_WAVES, 1) void br1l_kernel(
 // discipline of cmux_step3 on its own buffers (staging X1, digits X0 X1 X0 X1 X0 X1, inverse X0:
 // consecutive cross-wave uses alternate); the workgroup barriers are a superset of the group's,
 // and both groups run the same barrier sequence (a is uniform). Output: the blind rotation in the
-// coefficient domain, u64 [2][N2] (mode 1 of br2_trace_kernel); trace_kernel finishes mode 0.
+// coefficient domain, u64 [2][N2] (mode 1 of br2f_kernel); trace_kernel finishes mode 0.
 constexpr int BR2L_T = 2 * BR2_T;
 
 __global__ __launch_bounds__(BR2L_T, 1) void br2l_kernel(const uint32_t *__restrict__ lwe_int,
