@@ -168,9 +168,11 @@ def synthetic_payloads(first: int, count: int) -> np.ndarray:
 
 def rooflines(role, dom, launches, per_launch_msgs, launch_ms_total, value, world):
     """Dominant-kernel rooflines from HIP-event launch times and committed counter summaries.
-    The binding resource is FP64 VALU issue: `roofline` prices the kernel's FP64
-    FLOPs per launch (counted per message by rocprofv3 SQ_INSTS_VALU_*_F64, FMA = 2) against the
-    78.6 TFLOP/s FP64 peak. `hbm` gives the key-streaming figure of SURVEY.md §8(d) (every key
+    The blind rotations are VALU-issue and latency bound: `roofline` prices the
+    kernel's FP64 FLOPs per launch (counted per message by rocprofv3 SQ_INSTS_VALU_*_F64, FMA = 2)
+    against the 78.6 TFLOP/s FP64 peak, and carries the fractions of the VALU issue slots used by
+    its FP64 instructions and by all its VALU instructions (the level-2 FFT does 40 % fewer FLOPs
+    than round 2's NTT in 6 % less time, so its FLOP fraction is lower). `hbm` gives the key-streaming figure of SURVEY.md §8(d) (every key
     byte counted once per message: the north-star "fraction of HBM roofline") next to the HBM
     bytes the counters measured (FETCH_SIZE x 2 per the gfx950 correction + WRITE_SIZE)."""
     avg_launch_s = launch_ms_total / 1e3 / launches
@@ -194,6 +196,10 @@ def rooflines(role, dom, launches, per_launch_msgs, launch_ms_total, value, worl
                 "avg_launch_ms": round(avg_launch_s * 1e3, 2), "messages_per_launch": per_launch_msgs,
                 "fp64_lane_instr_frac": round(k["fp64_lane_instr_per_msg"] * per_launch_msgs / avg_launch_s
                                               / (FP64_PEAK_TFLOPS / 2 * 1e12), 4),
+                # every VALU instruction (FP64 or not) takes one issue slot of the same width: the
+                # fraction of the chip's VALU issue slots (at 2.4 GHz) the kernel used
+                "valu_issue_frac": round(k.get("valu_lane_instr_per_msg", 0.0) * per_launch_msgs / avg_launch_s
+                                         / (FP64_PEAK_TFLOPS / 2 * 1e12), 4),
                 "counts_from": comp.get("source")}
     return roof, hbm
 
