@@ -181,6 +181,11 @@ struct omr_ctx {
   uint32_t *x_flags = nullptr;
   int *x_err = nullptr, *x_err_host = nullptr;
   size_t x_cap = 0;
+  // multi-CU trace of the latency path (trace_x_kernel): partial slots [n][TRACE_X][2][2][N2],
+  // flags [n][TRACE_X]
+  double *t_slots = nullptr;
+  uint32_t *t_flags = nullptr;
+  size_t t_cap = 0;
   int num_cu = 0;
   bool coop = false;  // hipDeviceAttributeCooperativeLaunch
   // host-API staging
@@ -409,6 +414,8 @@ omr_status launch_br2x(omr_ctx *c, size_t n, const uint32_t *lwe_int, uint64_t *
     omr_status s;
     if ((s = scratch_idle(c)) != OMR_OK) return s;
     dev_free(c->x_slots);
+  dev_free(c->t_slots);
+  dev_free(c->t_flags);
     dev_free(c->x_flags);
     c->x_cap = 0;
     HIP_TRY(hipMalloc(&c->x_slots, n * 4 * N2 * sizeof(double)));
@@ -441,6 +448,46 @@ omr_status launch_br2x(omr_ctx *c, size_t n, const uint32_t *lwe_int, uint64_t *
   return OMR_OK;
 }
 
+// The latency path's trace over TRACE_X CUs per message (trace_x_kernel) as a cooperative launch;
+// false when refused (the caller then runs trace_kernel, one workgroup per message).
+omr_status launch_trace_x(omr_ctx *c, size_t n, uint64_t *io, hipStream_t st, bool *launched) {
+  *launched = false;
+  if (!c->coop || TRACE_X * n > 2 * (size_t)c->num_cu) return OMR_OK;
+  if (n > c->t_cap) {
+    omr_status s;
+    if ((s = scratch_idle(c)) != OMR_OK) return s;
+    dev_free(c->t_slots);
+    dev_free(c->t_flags);
+    c->t_cap = 0;
+    HIP_TRY(hipMalloc(&c->t_slots, n * TRACE_X * 4 * N2 * sizeof(double)));
+    HIP_TRY(hipMalloc(&c->t_flags, n * TRACE_X * sizeof(uint32_t)));
+    c->t_cap = n;
+  }
+  if (!c->x_err) {
+    HIP_TRY(hipMalloc(&c->x_err, sizeof(int)));
+    HIP_TRY(hipMemset(c->x_err, 0, sizeof(int)));
+    HIP_TRY(hipHostMalloc((void **)&c->x_err_host, sizeof(int), hipHostMallocDefault));
+    *c->x_err_host = 0;
+  }
+  HIP_TRY(hipMemsetAsync(c->t_flags, 0, n * TRACE_X * sizeof(uint32_t), st));
+  const double *tk = c->tk;
+  DeviceTables tb = c->tb;
+  double *slots = c->t_slots;
+  uint32_t *flags = c->t_flags;
+  int *err = c->x_err;
+  void *args[] = {(void *)&io, (void *)&tk, (void *)&tb, (void *)&slots, (void *)&flags, (void *)&err};
+  const hipError_t e = hipLaunchCooperativeKernel(reinterpret_cast<const void *>(&trace_x_kernel),
+                                                  dim3((unsigned)(TRACE_X * n)), dim3(BR2_T), args, 0, st);
+  if (e == hipErrorCooperativeLaunchTooLarge || e == hipErrorNotSupported || e == hipErrorInvalidConfiguration) {
+    (void)hipGetLastError();
+    return OMR_OK;
+  }
+  if (e != hipSuccess) return set_error(OMR_ERR_DEVICE, std::string("trace_x cooperative launch: ") + hipGetErrorString(e));
+  HIP_TRY(hipMemcpyAsync(c->x_err_host, c->x_err, sizeof(int), hipMemcpyDeviceToHost, st));
+  *launched = true;
+  return OMR_OK;
+}
+
 // Level-2 blind rotation (+ trace, mode 0) of n LWE(670, 4096) ciphertexts. `mid` (optional) is
 // recorded between the rotation and the trace; with split_trace (timing mode 2) the throughput
 // path runs them as two launches so that the event separates them.
@@ -459,7 +506,14 @@ omr_status launch_br2(omr_ctx *c, size_t n, const uint32_t *lwe_int, uint64_t *o
   HIP_TRY(hipGetLastError());
   if (mid) HIP_TRY(hipEventRecord(mid, st));
   if (split_trace && mode == 0) {
-    trace_kernel<<<(unsigned)n, BR2_T, 0, st>>>(out, c->tk, c->tb);
+    bool multi = false;
+#ifndef OMR_NO_TRACE_X
+    if (latency_path(c, n)) {
+      omr_status s;
+      if ((s = launch_trace_x(c, n, out, st, &multi)) != OMR_OK) return s;
+    }
+#endif
+    if (!multi) trace_kernel<<<(unsigned)n, BR2_T, 0, st>>>(out, c->tk, c->tb);
     HIP_TRY(hipGetLastError());
   }
   return OMR_OK;

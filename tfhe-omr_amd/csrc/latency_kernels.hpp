@@ -454,6 +454,157 @@ __global__ __launch_bounds__(BR2_T, 2) void trace_kernel(uint64_t *__restrict__ 
   hom_trace_store(acc0, acc1, xch, tws, xch + 2 * N, tk, tb, o, tid);
 }
 
+
+// hom_trace of the latency path over TRACE_X workgroups (CUs) per message (trace_x_kernel): every
+// workgroup keeps the mask and body (redundantly: the per-step updates are cheap), takes the 25
+// digits of sigma_g(a) and transforms and multiply-accumulates only digits d = w, w + TRACE_X, ...;
+// the partial sums (A, B), reduced, are all-reduced through global memory with br2x's rules (sc1
+// stores, vmcnt(0), barrier, one flag per workgroup carrying the step + 1, a bounded poll of every
+// partner's flag, sc1 loads; slot = step parity, reusable once every partner has published the
+// next step), then every workgroup applies B to the body (NTT domain) and INTT(A) to the mask.
+// Workgroup 0 stores NTT(c). The partials are canonicalised before the exchange, so their sum stays
+// below TRACE_X q / 2 < 2^53, and the residues are canonicalised as in hom_trace_store: the output
+// is bit-identical to it.
+// Global slots: xg[m][w][slot][A / B][N2] doubles; flags[m][w].
+#ifndef OMR_TRACE_X
+#define OMR_TRACE_X 5
+#endif
+constexpr int TRACE_X = OMR_TRACE_X;  // 25 digits: 5 per workgroup
+__global__ __launch_bounds__(BR2_T, 2) void trace_x_kernel(uint64_t *__restrict__ io, const double *__restrict__ tk,
+                                                           DeviceTables tb, double *xg, uint32_t *flags, int *err) {
+  using M = Mod<2>;
+  constexpr int T = BR2_T, E = BR2_E, N = N2;
+  using NTT = WgNtt<M, T, E>;
+  __shared__ double xch[NTT::LDS_DOUBLES];
+  __shared__ double tw[N], itw[N];
+  __shared__ int stop;
+  const int m = blockIdx.x / TRACE_X, w = blockIdx.x % TRACE_X;
+  const int tid = threadIdx.x;
+  uint64_t *o = io + (size_t)m * 2 * N;
+  constexpr double NINV = -549755813880.0;  // 2048^-1 mod q2, centred (hom_trace_store)
+  double ca[E], cb[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    ca[e] = canon<M>(mm<M>(from_u64<M>(o[tid + e * T]), NINV));
+    cb[e] = canon<M>(mm<M>(from_u64<M>(o[N + tid + e * T]), NINV));
+    tw[tid + e * T] = tb.tw2[tid + e * T];
+    itw[tid + e * T] = tb.itw2[tid + e * T];
+  }
+  if (tid == 0) stop = 0;
+  __syncthreads();
+  NTT::fwd(cb, xch, tw, tid);
+#pragma unroll
+  for (int e = 0; e < E; ++e) cb[e] = canon<M>(cb[e]);
+  uint32_t *fl = flags + (size_t)m * TRACE_X;
+#pragma unroll 1
+  for (int k = 0; k < TRACE_STEPS; ++k) {
+    const uint16_t *src = tb.trace_src + k * N;
+    const uint16_t *perm = tb.trace_perm + k * N;
+    uint32_t pk[E][DigitsTrace::DW];
+#pragma unroll
+    for (int e = 0; e < E; ++e) xch[tid + e * T] = ca[e];
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int sidx = src[tid + e * T];
+      DigitsTrace::pack(sidx < N ? xch[sidx] : -xch[sidx - N], pk[e]);  // sigma_g(a)
+    }
+    __syncthreads();
+    double accA[E], accB[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) accA[e] = accB[e] = 0.0;
+    const double *key = tk + (size_t)k * DT * 2 * N;
+    int cnt = 0;
+#pragma unroll 1
+    for (int d = w; d < DT; d += TRACE_X) {
+      const double *ka = key + (size_t)(d * 2) * N + tid * E;
+      const double *kb = ka + N;
+      double kra[E], krb[E];
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        kra[e] = ka[e];
+        krb[e] = kb[e];
+      }
+      double x[E];
+#pragma unroll
+      for (int e = 0; e < E; ++e) x[e] = DigitsTrace::get(pk[e], d);
+      NTT::fwd(x, xch, tw, tid);
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        accA[e] += mm<M>(x[e], kra[e]);
+        accB[e] += mm<M>(x[e], krb[e]);
+      }
+      if ((++cnt % 3) == 0) {
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          accA[e] = red<M>(accA[e]);
+          accB[e] = red<M>(accB[e]);
+        }
+      }
+    }
+    // all-reduce of the partials
+    const size_t slot = k & 1;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      accA[e] = red<M>(red<M>(accA[e]));  // canonical: TRACE_X of them sum below TRACE_X q / 2
+      accB[e] = red<M>(red<M>(accB[e]));
+      double *dst = xg + (((size_t)m * TRACE_X + w) * 2 + slot) * 2 * N + tid * E + e;
+      st_sc1(dst, accA[e]);
+      st_sc1(dst + N, accB[e]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      __hip_atomic_store(fl + w, (uint32_t)(k + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int p = 0; p < TRACE_X && !stop; ++p) {
+        if (p == w) continue;
+        int n = 0;
+        while (__hip_atomic_load(fl + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (uint32_t)(k + 1)) {
+          if (++n == BR2X_SPIN) {
+            stop = 1;
+            atomicExch(err, 1);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
+        }
+      }
+    }
+    __syncthreads();
+    if (stop) break;
+#pragma unroll
+    for (int p = 0; p < TRACE_X; ++p) {
+      if (p == w) continue;
+      const double *srcp = xg + (((size_t)m * TRACE_X + p) * 2 + slot) * 2 * N + tid * E;
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        accA[e] += ld_sc1(srcp + e);
+        accB[e] += ld_sc1(srcp + N + e);
+      }
+    }
+    // b_ntt += sigma_g(b)_ntt + B
+#pragma unroll
+    for (int e = 0; e < E; ++e) xch[tid * E + e] = cb[e];
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < E; ++e) cb[e] = canon<M>(cb[e] + xch[perm[tid * E + e]] + red<M>(accB[e]));
+    __syncthreads();
+    // a += INTT(A) (the sum of partials canonicalised first: a tighter input than the one-group trace's)
+#pragma unroll
+    for (int e = 0; e < E; ++e) accA[e] = red<M>(red<M>(accA[e]));
+    NTT::inv(accA, xch, itw, tid);
+#pragma unroll
+    for (int e = 0; e < E; ++e) ca[e] = canon<M>(ca[e] + accA[e]);
+  }
+  if (w != 0 || stop) return;
+  NTT::fwd(ca, xch, tw, tid);
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int t = tid * E + e;
+    o[t] = to_u64<M>(canon<M>(ca[e]));
+    o[N + t] = to_u64<M>(cb[e]);
+  }
+}
+
 }  // namespace omr
 
 #include "ks_mfma.hpp"
