@@ -162,12 +162,14 @@ omr_status omr_ctx_set_batch(omr_ctx *ctx, size_t batch);
 /* Chunks of at most `max_messages` messages run the latency kernels (each level-1 rotation
  * spread over more waves, each level-2 message over two CUs that exchange partial products
  * through global memory every step, or over two wave groups of one CU when the cooperative
- * launch of the two-CU grid is refused: lower single-message latency, bit-identical output);
- * larger chunks run the throughput kernels. Default 64; 0 = always throughput. The two-CU grid
- * is launched with hipLaunchCooperativeKernel, so its workgroups are co-resident; if a hand-off
- * still does not complete, the kernel ends, its output is invalid and the error is reported by
- * omr_ctx_check (after the caller's stream sync), by the host entry points, and by the next
- * detect call on the context (which then returns OMR_ERR_DEVICE without running). */
+ * launch of the two-CU grid is refused, and each message's trace over five CUs that all-reduce
+ * their digit partials, or one CU when that launch is refused: lower single-message latency,
+ * bit-identical output); larger chunks run the throughput kernels. Default 64; 0 = always
+ * throughput. The multi-CU grids are launched with hipLaunchCooperativeKernel, so their
+ * workgroups are co-resident; if a hand-off still does not complete, the kernel ends, its output
+ * is invalid and the error is reported by omr_ctx_check (after the caller's stream sync), by the
+ * host entry points, and by the next detect call on the context (which then returns
+ * OMR_ERR_DEVICE without running). */
 omr_status omr_ctx_set_latency_threshold(omr_ctx *ctx, size_t max_messages);
 /* Synchronises `hip_stream` (NULL: the whole device) and reports a pending device-side
  * failure of an earlier call on the context (the two-CU hand-off timeout above) as
