@@ -160,6 +160,7 @@ struct omr_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   double2 *bsk1f = nullptr;  // level-1 FFT-domain keys [512][8][2][512] complex, x 1/512
+  double2 *bsk1l = nullptr;  // the same in br1l_kernel's layout [512][8 slot][8 row][2][64 lane]
   double2 *fft1 = nullptr;   // level-1 FFT twiddles
   double *bsk2 = nullptr, *tk = nullptr;  // BSK2 NTT domain (latency kernels), trace key
   double2 *bsk2f = nullptr;                // BSK2 as FFT-domain 25-bit limbs (br2f_kernel), x 1/1024
@@ -396,7 +397,7 @@ omr_status launch_br1(omr_ctx *c, size_t n, const uint16_t *ca, const uint16_t *
                       const uint16_t *la, const uint16_t *lb, uint32_t *ext, uint64_t *rlwe, int mode,
                       hipStream_t st, size_t msgs) {
   if (latency_path(c, msgs))
-    br1l_kernel<<<(unsigned)n, 64 * BR1L_WAVES, 0, st>>>(ca, cb, la, lb, c->bsk1f, c->tb, ext, rlwe, mode);
+    br1l_kernel<<<(unsigned)n, 64 * BR1L_WAVES, 0, st>>>(ca, cb, la, lb, c->bsk1l, c->tb, ext, rlwe, mode);
   else
     br1f_kernel<<<(unsigned)((n + BR1F_WPG - 1) / BR1F_WPG), 64 * BR1F_WPG, 0, st>>>(
         ca, cb, la, lb, c->bsk1f, c->tb, ext, rlwe, mode, n);
@@ -613,6 +614,7 @@ extern "C" omr_status omr_ctx_create(const omr_detection_key_view *key, int devi
 
   // keys
   if (hipMalloc(&c->bsk1f, BSK1_ELEMS / 2 * sizeof(double2)) != hipSuccess ||
+      hipMalloc(&c->bsk1l, BSK1_ELEMS / 2 * sizeof(double2)) != hipSuccess ||
       hipMalloc(&c->bsk2, BSK2_ELEMS * sizeof(double)) != hipSuccess ||
       hipMalloc(&c->bsk2f, BSK2_ELEMS * sizeof(double2)) != hipSuccess ||
       hipMalloc(&c->tk, TK_ELEMS * sizeof(double)) != hipSuccess ||
@@ -622,6 +624,9 @@ extern "C" omr_status omr_ctx_create(const omr_detection_key_view *key, int devi
   omr_status st;
   if ((st = convert_keys_fft1(key->bsk1, BSK1_ELEMS / N1, c->bsk1f, c->fft1, c->stream)) != OMR_OK)
     return fail(st);
+  bsk1_latency_layout_kernel<<<(unsigned)(BSK1_ELEMS / 2 / 256), 256, 0, c->stream>>>(c->bsk1f, c->bsk1l,
+                                                                                     BSK1_ELEMS / 2);
+  if (hipGetLastError() != hipSuccess) return fail(set_error(OMR_ERR_DEVICE, "omr_ctx_create: BSK1 layout"));
   if ((st = convert_keys_cmux(key->bsk2, BSK2_ELEMS / N2, c->bsk2, ninv2, c->tb.tw2c, c->stream)) != OMR_OK)
     return fail(st);
   if ((st = convert_keys_fft2(key->bsk2, BSK2_ELEMS / N2, c->bsk2f, c->fft2, c->stream)) != OMR_OK) return fail(st);
@@ -650,6 +655,7 @@ extern "C" void omr_ctx_destroy(omr_ctx *c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->scratch_stream) (void)hipEventSynchronize(c->scratch_free);
   dev_free(c->bsk1f);
+  dev_free(c->bsk1l);
   dev_free(c->fft1);
   dev_free(c->bsk2);
   dev_free(c->bsk2f);
@@ -1151,3 +1157,15 @@ extern "C" omr_status omr_ntt(int level, int inverse, uint64_t *polys, size_t n,
   HIP_TRY(hipMemcpy(polys, dp.p, n * N * sizeof(uint64_t), hipMemcpyDeviceToHost));
   return OMR_OK;
 }
+
+#ifdef OMR_PHASE_TRACE
+// Debug builds only (tools/phase_trace.py): copy the latency kernels' phase timestamps.
+extern "C" int omr_debug_phase_read(unsigned long long *host, size_t n) {
+  const size_t cap = sizeof(omr::omr_phase_buf) / sizeof(unsigned long long);
+  if (n > cap) n = cap;
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(omr::omr_phase_buf), n * sizeof(unsigned long long)) == hipSuccess
+             ? (int)n
+             : -1;
+}
+#endif

@@ -414,7 +414,7 @@ struct CmuxNtt {
     double *buf = lds + XB * N;
 #pragma unroll
     for (int e = 0; e < E; ++e) buf[cmux_idx(PF, tid, e)] = x[e];
-    __syncthreads();
+    wg_barrier_lds();  // LDS only: the caller's key loads stay in flight across the exchange
 #pragma unroll
     for (int e = 0; e < E; ++e) x[e] = buf[cmux_idx(PT, tid, e)];
     __builtin_amdgcn_wave_barrier();  // keep the next writes below these reads (in-order LDS)

@@ -22,27 +22,68 @@
 
 namespace omr {
 
+// Phase timestamps of the latency kernels (tools/phase_trace.py; built only with
+// -DOMR_PHASE_TRACE): lane 0 of each traced wave stores clock64() at the phase boundaries of
+// executed steps PT_S0 .. PT_S0 + PT_STEPS - 1 (slots 0..7: br1l workgroup 0, waves 0..7; slots
+// 8..23: br2x workgroups 0, 1, waves 0..7), plus clock64 / wall_clock64 pairs at kernel entry and
+// exit for the clock rate.
+#ifdef OMR_PHASE_TRACE
+constexpr int PT_S0 = 200, PT_STEPS = 64, PT_K = 8, PT_SLOTS = 32;
+__device__ unsigned long long omr_phase_buf[PT_SLOTS * PT_STEPS * PT_K + PT_SLOTS * 4];
+__device__ __forceinline__ void phase_mark(int slot, int step, int k) {
+  if (slot >= 0 && (threadIdx.x & 63) == 0 && step >= PT_S0 && step < PT_S0 + PT_STEPS)
+    omr_phase_buf[(slot * PT_STEPS + (step - PT_S0)) * PT_K + k] = clock64();
+}
+__device__ __forceinline__ void phase_clock(int slot, int k) {  // k 0: entry, 1: exit
+  if (slot >= 0 && (threadIdx.x & 63) == 0) {
+    unsigned long long *p = omr_phase_buf + PT_SLOTS * PT_STEPS * PT_K + slot * 4 + 2 * k;
+    p[0] = clock64();
+    p[1] = wall_clock64();
+  }
+}
+#define OMR_PHASE(slot, step, k) phase_mark(slot, step, k)
+#define OMR_PHASE_CLOCK(slot, k) phase_clock(slot, k)
+#else
+#define OMR_PHASE(slot, step, k) ((void)0)
+#define OMR_PHASE_CLOCK(slot, k) ((void)0)
+#endif
+
 // ---- level 1 ---------------------------------------------------------------------------------
-// Level 1 over eight waves (one GGSW row each: wave w = p * D1 + k transforms digit k of
-// polynomial p, p = 0 mask, 1 body): each wave extracts one digit (16 coefficients instead of 32),
-// runs one forward FFT instead of two interleaved ones, and adds its products into the two output
-// sums in LDS with ds_add_f64 (the FFT product rounds to the exact integer whatever the summation
-// order, device_fft.hpp), so the partials need 16 KB instead of 64 KB. Waves 0 / 1 then read and
-// clear sum A / B, run its inverse and own the mask / body accumulator. Single-message level 1
-// 3.8 ms against 4.5 ms for four waves with two interleaved transforms each and partials summed
-// from LDS (profiles/r02j/latency_br1l_8wave_ab.log).
+// Level 1 over eight waves, one workgroup per rotation. Per CMUX step wave w = p * D1 + k extracts
+// digit k of polynomial p (p = 0 mask, 1 body: 16 coefficients per lane) and runs its forward FFT
+// (GGSW row w's digit spectrum); the eight spectra then cross through LDS (each wave's exchange
+// buffer, [e][lane]) and wave v multiplies the 8 spectra's register-slot-v points by the 8 rows'
+// keys (its slice of the step, the bsk1l layout: 16 KB contiguous per wave and step), producing
+// outputs A and B at those points with plain stores; waves 0 / 1 read output A / B, run its
+// inverse and own the mask / body accumulator. Three LDS-only barriers per step (the key loads of
+// the next executed step, issued after the multiply-accumulate, stay in flight across them).
+// Round 2's form summed the eight waves' products with ds_add_f64 atomics into shared sums: their
+// completion tail was ~3,600 cycles of a 17,100-cycle step (tools/phase_trace.py,
+// profiles/r03q/phase_br1l_atomics.log); the products now sum in registers in a fixed row order,
+// as in br1f_kernel, and the rounded FFT product is exact in either order (device_fft.hpp).
 constexpr int BR1L_WAVES = 2 * D1;
+
+// BSK1 rows [512][8 r][2 o][lane * 8 + e] -> the latency layout [512][8 e][8 r][2 o][64 lane]
+__global__ __launch_bounds__(256) void bsk1_latency_layout_kernel(const double2 *__restrict__ in,
+                                                                  double2 *__restrict__ out, size_t n) {
+  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= n) return;
+  const int lane = (int)(idx & 63), o = (int)((idx >> 6) & 1), r = (int)((idx >> 7) & 7), e = (int)((idx >> 10) & 7);
+  const size_t i = idx >> 13;
+  out[idx] = in[((i * 8 + r) * 2 + o) * 512 + lane * 8 + e];
+}
 
 __global__ __launch_bounds__(64 * BR1L_WAVES, 1) void br1l_kernel(
     const uint16_t *__restrict__ clue_a, const uint16_t *__restrict__ clue_b,
     const uint16_t *__restrict__ lwe_a, const uint16_t *__restrict__ lwe_b,
-    const double2 *__restrict__ bskf, DeviceTables tb, uint32_t *__restrict__ ext_out,
+    const double2 *__restrict__ bskl, DeviceTables tb, uint32_t *__restrict__ ext_out,
     uint64_t *__restrict__ rlwe_out, int mode) {
   using F = Fft512;
   constexpr int NF = F::N, W = BR1L_WAVES;
+  static_assert(W == 8 && NF == 8 * 64, "one wave per GGSW row and per register slot");
   __shared__ int ext[2][2 * N1];              // [ACC, -ACC] per poly (0 mask, 1 body)
-  __shared__ double2 xch_all[W][F::BUF];      // per wave: one transform
-  __shared__ double sum[2][2][8 * 64];        // outputs A, B: [re, im][slot e * 64 + lane]
+  __shared__ double2 xch_all[W][F::BUF];      // per wave: its transform's exchange, then its spectrum [e][lane]
+  __shared__ double2 outs[2][8 * 64];         // outputs A, B: [e][lane]
   __shared__ double2 tws[NF];
   __shared__ uint16_t la[N0];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -75,31 +116,31 @@ __global__ __launch_bounds__(64 * BR1L_WAVES, 1) void br1l_kernel(
     }
   }
   for (int j = threadIdx.x; j < NF; j += 64 * W) tws[j] = tb.fft1[j];
-  for (int j = threadIdx.x; j < 2 * 2 * 8 * 64; j += 64 * W) (&sum[0][0][0])[j] = 0.0;
   __syncthreads();
-  // GGSW row `wave` of the next executed step is loaded one step ahead (issued after this step's
-  // multiply-accumulate, in flight across the inverse and the next digits + transform): a lone
-  // message's rows come from HBM / the Infinity Cache, and a step takes ~7 us.
+  // Wave v's key slice of an executed step: rows 0..7, outputs A / B at register slot v of every
+  // lane (16 KB contiguous per wave), loaded two executed steps ahead (below).
   auto next_step = [&](int i) {  // first i' >= i with a_i' != 0 (uniform)
     while (i < N0 && la[i] == 0) ++i;
     return i;
   };
-  double2 kk[2][8];  // [output A/B][point]
-  auto load_row = [&](int i) {
+  double2 kk0[8][2], kk1[8][2];  // [row][output A/B] of two consecutive executed steps
+  auto load_slice = [&](double2 (&kk)[8][2], int i) {
     if (i >= N0) return;
-    const double2 *kr = bskf + ((size_t)i * 2 * D1 + wave) * 2 * NF + lane * 8;  // GGSW row `wave`
+    const double2 *kr = bskl + ((size_t)i * 8 + wave) * 16 * 64 + lane;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      kk[0][e] = kr[e];
-      kk[1][e] = kr[NF + e];
-    }
+    for (int r = 0; r < 8; ++r)
+#pragma unroll
+      for (int o = 0; o < 2; ++o) kk[r][o] = kr[(r * 2 + o) * 64];
   };
-  int i = next_step(0), inext;
-  load_row(i);
-#pragma unroll 1
-  for (; i < N0; i = inext) {
+  const int pslot = __builtin_amdgcn_readfirstlane(blockIdx.x == 0 ? wave : -1);
+  int hs = 0;
+  (void)pslot;
+  (void)hs;
+  // one CMUX step at executed step i with its key slice kk (kko: the other slice buffer; inext,
+  // inext2: the next two executed steps)
+  auto cmux = [&](int i, double2 (&kk)[8][2], double2 (&kko)[8][2], int inext, int inext2) {
     const int a = __builtin_amdgcn_readfirstlane(la[i]);  // != 0: (X^0 - 1) * ACC = 0 is skipped
-    inext = __builtin_amdgcn_readfirstlane(next_step(i + 1));
+    OMR_PHASE(pslot, hs, 0);
     double xr[1][8], xi[1][8];
     const int base = lane - a + 2 * N1;
 #pragma unroll
@@ -112,28 +153,48 @@ __global__ __launch_bounds__(64 * BR1L_WAVES, 1) void br1l_kernel(
       else
         xi[0][q - 8] = d;
     }
+    OMR_PHASE(pslot, hs, 1);
     F::fwd<1, true>(xr, xi, xch, tws, lane, tb.fft1);
+    wave_lds_fence();  // the spectrum's writes stay below the transform's exchange reads
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+    for (int e = 0; e < 8; ++e) xch[e * 64 + lane] = make_double2(xr[0][e], xi[0][e]);
+    OMR_PHASE(pslot, hs, 2);
+    // waves 0 / 1 (the inverses' critical path) load the next step's slice here, in the time they
+    // wait for waves 4..7, which share their SIMDs and finish their transforms ~2,500 cycles later
+    if (wave < 2) load_slice(kko, inext);
+    wg_barrier_lds();  // every spectrum is in LDS
+    OMR_PHASE(pslot, hs, 3);
+    {  // outputs A, B at register slot `wave` of every lane: rows in order, as br1f_step_lds
+      double ar = 0.0, ai = 0.0, br = 0.0, bi = 0.0;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const double re = __fma_rn(xr[0][e], kk[t][e].x, -xi[0][e] * kk[t][e].y);
-        const double im = __fma_rn(xr[0][e], kk[t][e].y, xi[0][e] * kk[t][e].x);
-        __hip_atomic_fetch_add(&sum[t][0][e * 64 + lane], re, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        __hip_atomic_fetch_add(&sum[t][1][e * 64 + lane], im, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      for (int r = 0; r < 8; ++r) {
+        const double2 x = xch_all[r][wave * 64 + lane];
+        const double2 ka = kk[r][0], kB = kk[r][1];
+        ar = __fma_rn(x.x, ka.x, __fma_rn(-x.y, ka.y, ar));
+        ai = __fma_rn(x.x, ka.y, __fma_rn(x.y, ka.x, ai));
+        br = __fma_rn(x.x, kB.x, __fma_rn(-x.y, kB.y, br));
+        bi = __fma_rn(x.x, kB.y, __fma_rn(x.y, kB.x, bi));
       }
-    load_row(inext);
-    __syncthreads();
+      outs[0][wave * 64 + lane] = make_double2(ar, ai);
+      outs[1][wave * 64 + lane] = make_double2(br, bi);
+    }
+    wg_barrier_lds();  // outputs complete; every spectrum read (the exchange buffers are free)
+    OMR_PHASE(pslot, hs, 4);
+    // waves 2..7: the slice two executed steps ahead, into the registers just consumed, issued
+    // while waves 0 / 1 run the inverses (issuing 16 KB per wave before the barrier above held
+    // every wave there ~2,300 cycles)
+    if (wave >= 2) load_slice(kk, inext2);
     if (wave < 2) {  // wave 0: output A (mask accumulator), wave 1: output B (body accumulator)
       double sr[1][8], si[1][8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        sr[0][e] = sum[wave][0][e * 64 + lane];
-        si[0][e] = sum[wave][1][e * 64 + lane];
-        sum[wave][0][e * 64 + lane] = 0.0;  // cleared for the next step (after the barrier below)
-        sum[wave][1][e * 64 + lane] = 0.0;
+        const double2 v = outs[wave][e * 64 + lane];
+        sr[0][e] = v.x;
+        si[0][e] = v.y;
       }
+      OMR_PHASE(pslot, hs, 5);
       F::inv<1, true>(sr, si, xch, tws, lane, tb.fft1);
+      OMR_PHASE(pslot, hs, 6);
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const double v = rint(q < 8 ? sr[0][q] : si[0][q - 8]);  // exact (< 2^43)
@@ -142,8 +203,27 @@ __global__ __launch_bounds__(64 * BR1L_WAVES, 1) void br1l_kernel(
         ext[wave][N1 + acc_coef(lane, q)] = -ac[q];
       }
     }
-    __syncthreads();
+    wg_barrier_lds();  // ACC staged for the next step's digits
+    OMR_PHASE(pslot, hs, 7);
+    ++hs;
+  };
+  // key slices alternate between kk0 and kk1: waves 2..7 load each two executed steps ahead,
+  // waves 0 / 1 one step ahead (before the first barrier of the step in between)
+  int i0 = next_step(0), i1 = next_step(i0 + 1);
+  load_slice(kk0, i0);
+  if (wave >= 2) load_slice(kk1, i1);
+  OMR_PHASE_CLOCK(pslot, 0);
+#pragma unroll 1
+  while (i0 < N0) {
+    const int i2 = __builtin_amdgcn_readfirstlane(next_step(i1 + 1));
+    cmux(i0, kk0, kk1, i1, i2);
+    if (i1 >= N0) break;
+    const int i3 = __builtin_amdgcn_readfirstlane(next_step(i2 + 1));
+    cmux(i1, kk1, kk0, i2, i3);
+    i0 = i2;
+    i1 = i3;
   }
+  OMR_PHASE_CLOCK(pslot, 1);
   if (mode == 0) {  // extract_lwe_locally (coefficient 0), detector.rs:561
     uint32_t *o = ext_out + g * (N1 + 1);
     for (int j = threadIdx.x; j < N1; j += 64 * W) o[j] = Lvl1Int::to_u32(j == 0 ? ext[0][0] : -ext[0][N1 - j]);
@@ -334,10 +414,14 @@ __global__ __launch_bounds__(BR2L_T, 1) void br2x_kernel(const uint32_t *__restr
   }
   uint32_t *my_flag = flags + 2 * m + r, *their_flag = flags + 2 * m + (1 - r);
   uint32_t hc = 0;  // hand-offs so far (executed steps)
+  const int pslot = __builtin_amdgcn_readfirstlane(blockIdx.x < 2 ? 8 + 8 * (int)blockIdx.x + (int)(threadIdx.x >> 6) : -1);
+  (void)pslot;
+  OMR_PHASE_CLOCK(pslot, 0);
 #pragma unroll 1
   for (int i = 0; i < NI; ++i) {
     const int a = (int)__builtin_amdgcn_readfirstlane(lwe[i]) & (2 * N - 1);
     if (a == 0) continue;  // (X^0 - 1) * ACC = 0 (both workgroups of the message skip it)
+    OMR_PHASE(pslot, (int)hc, 0);
     const size_t slot = hc & 1;
     const double *ggsw = bsk2 + ((size_t)i * 2 * D2 + (size_t)r * D2 + (size_t)g * KD) * 2 * N;
     uint32_t pk[E][DG::DW];
@@ -353,6 +437,7 @@ __global__ __launch_bounds__(BR2L_T, 1) void br2x_kernel(const uint32_t *__restr
       __builtin_amdgcn_wave_barrier();
       __atomic_signal_fence(__ATOMIC_SEQ_CST);
     }
+    OMR_PHASE(pslot, (int)hc, 1);
     double accA[E], accB[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) accA[e] = accB[e] = 0.0;
@@ -385,6 +470,7 @@ __global__ __launch_bounds__(BR2L_T, 1) void br2x_kernel(const uint32_t *__restr
       }
     }
     __syncthreads();
+    OMR_PHASE(pslot, (int)hc, 3);
     double keep[E];
     if (g == 0) {
 #pragma unroll
@@ -397,6 +483,7 @@ __global__ __launch_bounds__(BR2L_T, 1) void br2x_kernel(const uint32_t *__restr
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
+    OMR_PHASE(pslot, (int)hc, 4);
     if (threadIdx.x == 0) {
       __hip_atomic_store(my_flag, hc + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       int n = 0;
@@ -410,6 +497,7 @@ __global__ __launch_bounds__(BR2L_T, 1) void br2x_kernel(const uint32_t *__restr
       }
     }
     __syncthreads();
+    OMR_PHASE(pslot, (int)hc, 5);
     if (stop) break;
     if (g == 0) {
       double s[E];
@@ -417,13 +505,17 @@ __global__ __launch_bounds__(BR2L_T, 1) void br2x_kernel(const uint32_t *__restr
       for (int e = 0; e < E; ++e)
         s[e] = red<M>(keep[e] + ld_sc1(xg + (((size_t)m * 2 + (1 - r)) * 2 + slot) * N + t * E + e));
       NTT::template inv<0>(s, X, tw, t, tb.tw2c);
+      OMR_PHASE(pslot, (int)hc, 6);
 #pragma unroll
       for (int e = 0; e < E; ++e) acc[e] = canon<M>(acc[e] + s[e]);
     } else {
       __syncthreads();  // the inverse's one workgroup barrier (its cross-wave exchange)
+      OMR_PHASE(pslot, (int)hc, 6);
     }
+    OMR_PHASE(pslot, (int)hc, 7);
     ++hc;
   }
+  OMR_PHASE_CLOCK(pslot, 1);
   if (g == 0) {
     uint64_t *o = out + (size_t)m * 2 * N + (size_t)r * N;
 #pragma unroll

@@ -1,0 +1,46 @@
+"""Per-phase durations of the latency kernels from a -DOMR_PHASE_TRACE build
+(tools/build_variant.sh phase -DOMR_PHASE_TRACE; OMR_GPU_LIB=.../var_phase.so python tools/phase_trace.py).
+Runs one single-message detect (latency path) and prints the mean cycles between consecutive phase
+marks of executed steps 200..263 for every traced wave (br1l workgroup 0; br2x workgroups 0, 1)."""
+import ctypes
+import sys
+
+sys.path.insert(0, "tests")
+import numpy as np  # noqa: E402
+
+import product_lib as PL  # noqa: E402
+from product_lib import omr_amd as A  # noqa: E402
+
+PT_STEPS, PT_K, PT_SLOTS = 64, 8, 32
+a, b, dk = PL.keys()
+det = A.Detector(dk)
+ca, cb = a.gen_clues(1000, 0, 256)
+det.detect_batch(ca[:1], cb[:1])
+det.detect_batch(ca[1:2], cb[1:2])
+n = PT_SLOTS * PT_STEPS * PT_K + PT_SLOTS * 4
+buf = (ctypes.c_ulonglong * n)()
+lib = A.lib()
+lib.omr_debug_phase_read.restype = ctypes.c_int
+got = lib.omr_debug_phase_read(buf, ctypes.c_size_t(n))
+assert got == n, got
+arr = np.frombuffer(buf, dtype=np.uint64).astype(np.int64)
+marks = arr[: PT_SLOTS * PT_STEPS * PT_K].reshape(PT_SLOTS, PT_STEPS, PT_K)
+clk = arr[PT_SLOTS * PT_STEPS * PT_K:].reshape(PT_SLOTS, 4)
+names = {
+    "br1l": ["digits", "fwd + spectrum store", "barrier1", "mac + stores + barrier2", "outs read", "inverse", "update + barrier3"],
+    "br2x": ["stage+digits", "3 fwd + MAC + g1 partial + barrier", "g0 sum + sc1 stores + vmcnt + barrier",
+             "flag + poll + barrier", "sc1 loads + inverse", "update"],
+}
+for slot in range(24):
+    kern = "br1l" if slot < 8 else "br2x"
+    m = marks[slot]
+    if not m[:, 0].any():
+        continue
+    c0, w0, c1, w1 = clk[slot]
+    mhz = (c1 - c0) / ((w1 - w0) / 100.0) if w1 > w0 else float("nan")
+    step = np.diff(m[:, 0]).mean() if PT_STEPS > 1 else 0
+    d = np.diff(m, axis=1).mean(axis=0)
+    lab = f"{kern} wg{(slot - 8) // 8 if slot >= 8 else 0} wave{slot % 8}"
+    parts = "  ".join(f"{nm} {v:.0f}" for nm, v in zip(names[kern], d) if v > 0)
+    print(f"{lab}: clock {mhz:.0f} MHz, step {step:.0f} cyc ({step / mhz:.2f} us) | {parts}", flush=True)
+det.close()
