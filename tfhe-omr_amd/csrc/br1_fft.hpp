@@ -122,6 +122,11 @@ __device__ __forceinline__ void br1f_digits(const uint32_t (&ac)[2][16], uint32_
 // next row's copy in flight across the barriers (cdna_hip_programming.md, "Pipelining across
 // barriers").
 constexpr int KROW_SLOTS = 2 * Fft512::N;  // double2 per staged row
+
+// Storage position of transform point (lane, e) within a BSK1 key polynomial: register-major, so
+// that each LDS-DMA instruction of krow_issue copies 1 KB contiguous (lane-major, 16 B per lane at
+// a 128 B stride: level 1 1 % slower, profiles/r03q/key_layout_ab.log).
+__device__ __forceinline__ int key1_pos(int lane, int e) { return e * 64 + lane; }
 constexpr int KROW_INSTR = 16 / BR1F_WPG;  // glds per wave per row
 
 __device__ __forceinline__ void krow_issue(const double2 *__restrict__ row, double2 *buf, int lane,
@@ -130,7 +135,7 @@ __device__ __forceinline__ void krow_issue(const double2 *__restrict__ row, doub
   for (int u = 0; u < KROW_INSTR; ++u) {
     const int ins = wave * KROW_INSTR + u;  // 0..15: comp = ins / 8, point e = ins % 8
     const int comp = ins >> 3, e = ins & 7;
-    const double2 *src = row + comp * Fft512::N + lane * 8 + e;
+    const double2 *src = row + comp * Fft512::N + key1_pos(lane, e);
     __builtin_amdgcn_global_load_lds(src, buf + comp * Fft512::N + e * 64, 16, 0, 0);
   }
 }
@@ -289,9 +294,9 @@ __global__ __launch_bounds__(64) void key_to_fft1_kernel(const uint32_t *__restr
   }
   __syncthreads();
   F::fwd(xr, xi, xch, tws, lane);
-  double2 *dst = out + poly * F::N + lane * 8;
+  double2 *dst = out + poly * F::N;
 #pragma unroll
-  for (int e = 0; e < 8; ++e) dst[e] = make_double2(xr[e] * (1.0 / 512), xi[e] * (1.0 / 512));
+  for (int e = 0; e < 8; ++e) dst[key1_pos(lane, e)] = make_double2(xr[e] * (1.0 / 512), xi[e] * (1.0 / 512));
 }
 
 // Test entry (omr_fft1_mul): out = a * k mod (X^1024 + 1, q1) through the level-1 FFT path,

@@ -230,8 +230,15 @@ struct Fft1024 {
 
 constexpr double LIMB = 33554432.0;  // 2^25: key = lo + 2^25 hi
 
+// Storage position of point 4 t + e (P4 layout: thread t's register e) within a key block:
+// register-major, so that each of a thread's four loads per block is one 1 KB-contiguous wave
+// instruction (16 B per lane). The point-major order (4 t + e: 64 B per thread, 16 B per lane at a
+// 64 B stride per instruction) ran level 2 8.7 % slower: 667 vs 609 ms per 16,384 messages
+// (profiles/r03q/key_layout_ab.log).
+__device__ __forceinline__ int key_pos(int t, int e) { return e * Fft1024::T + t; }
+
 // BSK2 rows (canonical u64 [670][12][2][2048]) -> FFT-domain limbs, x 1/1024:
-// out double2 [670][12][2 out][2 limb][1024] at position 4 t + e (Fft1024's P4 layout).
+// out double2 [670][12][2 out][2 limb][1024], point 4 t + e (Fft1024's P4 layout) at key_pos(t, e).
 __global__ __launch_bounds__(256) void key_to_fft2_kernel(const uint64_t *__restrict__ in, double2 *__restrict__ out,
                                                           size_t npoly, const double2 *__restrict__ twg) {
   using F = Fft1024;
@@ -261,9 +268,10 @@ __global__ __launch_bounds__(256) void key_to_fft2_kernel(const uint64_t *__rest
   for (int l = 0; l < 2; ++l) {
     F::fwd(lr[l], li[l], X, W, tws, t);
     __syncthreads();  // X is reused by the next limb's exchange
-    double2 *dst = out + (poly * 2 + l) * F::n + 4 * t;
+    double2 *dst = out + (poly * 2 + l) * F::n;
 #pragma unroll
-    for (int e = 0; e < F::E; ++e) dst[e] = make_double2(lr[l][e] * (1.0 / F::n), li[l][e] * (1.0 / F::n));
+    for (int e = 0; e < F::E; ++e)
+      dst[key_pos(t, e)] = make_double2(lr[l][e] * (1.0 / F::n), li[l][e] * (1.0 / F::n));
   }
 }
 
@@ -318,7 +326,7 @@ __global__ __launch_bounds__(256, 2) void br2f_kernel(const uint32_t *__restrict
 #pragma unroll
     for (int l = 0; l < 2; ++l)
 #pragma unroll
-      for (int e = 0; e < E; ++e) k[l][e] = row[(o * 2 + l) * F::n + 4 * t + e];
+      for (int e = 0; e < E; ++e) k[l][e] = row[(o * 2 + l) * F::n + key_pos(t, e)];
   };
   constexpr size_t ROW = 4 * F::n;  // double2 per GGSW row
 #pragma unroll 1

@@ -70,7 +70,7 @@ __global__ __launch_bounds__(256) void bsk1_latency_layout_kernel(const double2 
   if (idx >= n) return;
   const int lane = (int)(idx & 63), o = (int)((idx >> 6) & 1), r = (int)((idx >> 7) & 7), e = (int)((idx >> 10) & 7);
   const size_t i = idx >> 13;
-  out[idx] = in[((i * 8 + r) * 2 + o) * 512 + lane * 8 + e];
+  out[idx] = in[((i * 8 + r) * 2 + o) * 512 + key1_pos(lane, e)];
 }
 
 __global__ __launch_bounds__(64 * BR1L_WAVES, 1) void br1l_kernel(
