@@ -72,8 +72,23 @@ TW_LEN = 3 * (4 + 16 + 64 + 256)
 
 
 def tw_addr(p, t, k):
-    """Table slot (double2) of twiddle k (0 B, 1 A, 2 AB) of thread t's block in pass p."""
+    """Global-table (host order) slot (double2) of twiddle k (0 B, 1 A, 2 AB) of thread t's block."""
     return TW_OFF[p] + 3 * tw_index(p, t) + k
+
+
+def tw_slot(p, b, k):
+    """LDS slot of twiddle k of block b (Fft1024::tw_slot): passes 3 and 4 keep each k in its own
+    array with the block XOR-swizzled."""
+    if p == 3:
+        return TW_OFF[3] + k * 64 + (b ^ (((b >> 4) & 3) << 1))
+    if p == 4:
+        return TW_OFF[4] + k * 256 + (b ^ (((b >> 6) & 3) << 2))
+    return TW_OFF[p] + 3 * b + k
+
+
+def tw_lds(p, t, k):
+    """LDS slot of twiddle k of thread t's block in pass p."""
+    return tw_slot(p, tw_index(p, t), k)
 
 
 def twiddle_table():

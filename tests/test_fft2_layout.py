@@ -50,16 +50,22 @@ def test_twiddle_table_layout():
 
 
 def test_twiddle_read_cycles():
-    """The block-major table's ds_read_b128 twiddle reads: conflict-free (4 cycles per wave
-    instruction) in passes 1 and 2, 4-way conflicts (16) in passes 3 and 4. A permuted table that
-    removes them (SQ_LDS_BANK_CONFLICT 9.8e10 -> 3.5e8 cycles per 16,384 messages) measured 11 %
-    SLOWER end to end: the workgroups drifted further apart in CMUX step and the L2 misses on the
-    key rows grew 5x (level-2 measurements), so the device keeps this layout."""
-    cyc = {}
+    """ds_read_b128 twiddle reads: the host (block-major) order has 4-way conflicts (16 cycles per
+    wave instruction) in passes 3 and 4; the LDS slots of Fft1024::tw_slot (each twiddle of passes
+    3 and 4 in its own array, the block XOR-swizzled) are conflict-free (4) in every pass. (With
+    the point-major key layout a permuted table measured 11 % slower, the workgroups drifting apart
+    in CMUX step; with the register-major keys this one is 0.8 % faster) The
+    slots are a permutation of the table."""
+    host, lds = {}, {}
     for p in range(1, 5):
-        cyc[p] = max(M.lds_cycles([M.tw_addr(p, w * 64 + l, k) * 16 for l in range(64)], M.READ_B128, 64, 16)
+        host[p] = max(M.lds_cycles([M.tw_addr(p, w * 64 + l, k) * 16 for l in range(64)], M.READ_B128, 64, 16)
+                      for w in range(4) for k in range(3))
+        lds[p] = max(M.lds_cycles([M.tw_lds(p, w * 64 + l, k) * 16 for l in range(64)], M.READ_B128, 64, 16)
                      for w in range(4) for k in range(3))
-    assert cyc == {1: 4, 2: 4, 3: 16, 4: 16}
+    assert host == {1: 4, 2: 4, 3: 16, 4: 16}
+    assert lds == {1: 4, 2: 4, 3: 4, 4: 4}
+    slots = sorted(M.tw_slot(p, b, k) for p in range(1, 5) for b in range(4 ** p) for k in range(3))
+    assert slots == list(range(M.TW_LEN))
     # pass-0 constants of the device code: B = e^{i pi/8}, A = e^{i pi/4}, AB = e^{3 i pi/8}
     B, A, AB = M.block_tw(0, 0)
     assert np.allclose([B, A, AB], np.exp(1j * np.pi * np.array([1, 2, 3]) / 8))

@@ -31,7 +31,7 @@ namespace omr {
 struct Fft1024 {
   static constexpr int T = 256, E = 4, n = 1024, L = 10;
   static constexpr int TW_LEN = 3 * (4 + 16 + 64 + 256);  // passes 1..4: (B, A, AB) per block
-  __device__ static constexpr int tw_off(int p) { return p == 1 ? 0 : p == 2 ? 12 : p == 3 ? 60 : 252; }
+  OMR_HD static constexpr int tw_off(int p) { return p == 1 ? 0 : p == 2 ? 12 : p == 3 ? 60 : 252; }
 
   // index bit of each position bit (e1, e0, l5, l4, l3, l2, l1, l0, w1, w0), per pass layout
   OMR_HD static constexpr int lay(int p, int k) {
@@ -117,6 +117,23 @@ struct Fft1024 {
   __device__ static __forceinline__ int block(int t) {
     return idx(P, t, 0) >> (L - 2 * P);
   }
+  // LDS slot of twiddle k (0 B, 1 A, 2 AB) of block b in pass P. The global table (host order) is
+  // tw_off(P) + 3 b + k, whose ds_read_b128 reads conflict 4-way in passes 3 and 4; there each k
+  // has its own array with the block XOR-swizzled, conflict-free (tests/test_fft2_layout.py::
+  // test_twiddle_read_cycles; level 2 0.8 % faster, profiles/r03q/twiddle_soa_ab.log).
+  OMR_HD static constexpr int tw_slot(int P, int b, int k) {
+    return P == 3 ? tw_off(3) + k * 64 + (b ^ (((b >> 4) & 3) << 1))
+         : P == 4 ? tw_off(4) + k * 256 + (b ^ (((b >> 6) & 3) << 2))
+                  : tw_off(P) + 3 * b + k;
+  }
+  // the global table (host order) into LDS slots
+  __device__ static __forceinline__ void load_twiddles(double2 *tws, const double2 *__restrict__ twg, int t) {
+    for (int j = t; j < TW_LEN; j += T) {
+      const int P = j < tw_off(2) ? 1 : j < tw_off(3) ? 2 : j < tw_off(4) ? 3 : 4;
+      const int r = j - tw_off(P);
+      tws[tw_slot(P, r / 3, r % 3)] = twg[j];
+    }
+  }
   template <int P>
   __device__ static __forceinline__ void fwd_pass(double (&xr)[E], double (&xi)[E], const double2 *tws, int t) {
     if constexpr (P == 0) {
@@ -124,8 +141,8 @@ struct Fft1024 {
       cmul(xr[2], xi[2], R2, R2);
       cmul(xr[3], xi[3], S8, C8);
     } else {
-      const double2 *w = tws + tw_off(P) + 3 * block<P>(t);
-      const double2 B = w[0], A = w[1], AB = w[2];
+      const int b = block<P>(t);
+      const double2 B = tws[tw_slot(P, b, 0)], A = tws[tw_slot(P, b, 1)], AB = tws[tw_slot(P, b, 2)];
       cmul(xr[1], xi[1], B.x, B.y);
       cmul(xr[2], xi[2], A.x, A.y);
       cmul(xr[3], xi[3], AB.x, AB.y);
@@ -140,8 +157,8 @@ struct Fft1024 {
       cmulc(xr[2], xi[2], R2, R2);
       cmulc(xr[3], xi[3], S8, C8);
     } else {
-      const double2 *w = tws + tw_off(P) + 3 * block<P>(t);
-      const double2 B = w[0], A = w[1], AB = w[2];
+      const int b = block<P>(t);
+      const double2 B = tws[tw_slot(P, b, 0)], A = tws[tw_slot(P, b, 1)], AB = tws[tw_slot(P, b, 2)];
       cmulc(xr[1], xi[1], B.x, B.y);
       cmulc(xr[2], xi[2], A.x, A.y);
       cmulc(xr[3], xi[3], AB.x, AB.y);
@@ -248,7 +265,7 @@ __global__ __launch_bounds__(256) void key_to_fft2_kernel(const uint64_t *__rest
   const int t = threadIdx.x;
   const size_t poly = blockIdx.x;
   if (poly >= npoly) return;
-  for (int j = t; j < F::TW_LEN; j += F::T) tws[j] = twg[j];
+  F::load_twiddles(tws, twg, t);
   const uint64_t *src = in + poly * N2;
   double lr[2][F::E], li[2][F::E];  // [limb][point]
 #pragma unroll
@@ -301,7 +318,7 @@ __global__ __launch_bounds__(256, 2) void br2f_kernel(const uint32_t *__restrict
   double2 *W = lds2[2];
   const int t = threadIdx.x;
   const uint32_t *lwe = lwe_int + (size_t)blockIdx.x * (NI + 1);
-  for (int j = t; j < F::TW_LEN; j += F::T) tws[j] = twg[j];
+  F::load_twiddles(tws, twg, t);
   // ACC = (0, X^{-b} * LUT2): ac[p][h][e] = coefficient idx(0, t, e) + 1024 h of poly p
   double ac[2][2][E];
   {

@@ -353,6 +353,8 @@ __global__ __launch_bounds__(BR2L_T, 1) void br2l_kernel(const uint32_t *__restr
 // output the partner owns (mask CU: B, body CU: A) crosses to it through global memory and the
 // partner's arrives the same way; group 0 runs the inverse transform and updates ACC_r. Half the
 // transforms of br2l_kernel per CU and step, plus one hand-off.
+// The hand-off slots are lane-contiguous (register e of thread t at e * 256 + t): each 8 B sc1 store
+// or load instruction covers 512 B of four whole lines (profiles/r03q/handoff_layout_ab.log).
 // Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility, the first row of the sc1 table):
 // every storing thread stores its payload with sc1 stores (agent-scope relaxed atomics) and waits
 // vmcnt(0); a workgroup barrier; one lane stores the sc1 flag (step + 1). The consumer's lane 0
@@ -478,7 +480,7 @@ __global__ __launch_bounds__(BR2L_T, 1) void br2x_kernel(const uint32_t *__restr
         const double sa = red<M>(red<M>(accA[e]) + part[0][t * E + e]);
         const double sb = red<M>(red<M>(accB[e]) + part[1][t * E + e]);
         keep[e] = r == 0 ? sa : sb;
-        st_sc1(xg + (((size_t)m * 2 + r) * 2 + slot) * N + t * E + e, r == 0 ? sb : sa);  // the partner's output
+        st_sc1(xg + (((size_t)m * 2 + r) * 2 + slot) * N + e * T + t, r == 0 ? sb : sa);  // the partner's output
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -503,7 +505,7 @@ __global__ __launch_bounds__(BR2L_T, 1) void br2x_kernel(const uint32_t *__restr
       double s[E];
 #pragma unroll
       for (int e = 0; e < E; ++e)
-        s[e] = red<M>(keep[e] + ld_sc1(xg + (((size_t)m * 2 + (1 - r)) * 2 + slot) * N + t * E + e));
+        s[e] = red<M>(keep[e] + ld_sc1(xg + (((size_t)m * 2 + (1 - r)) * 2 + slot) * N + e * T + t));
       NTT::template inv<0>(s, X, tw, t, tb.tw2c);
       OMR_PHASE(pslot, (int)hc, 6);
 #pragma unroll
@@ -640,7 +642,7 @@ __global__ __launch_bounds__(BR2_T, 2) void trace_x_kernel(uint64_t *__restrict_
     for (int e = 0; e < E; ++e) {
       accA[e] = red<M>(red<M>(accA[e]));  // canonical: TRACE_X of them sum below TRACE_X q / 2
       accB[e] = red<M>(red<M>(accB[e]));
-      double *dst = xg + (((size_t)m * TRACE_X + w) * 2 + slot) * 2 * N + tid * E + e;
+      double *dst = xg + (((size_t)m * TRACE_X + w) * 2 + slot) * 2 * N + e * T + tid;  // lane-contiguous: 512 B per store instruction
       st_sc1(dst, accA[e]);
       st_sc1(dst + N, accB[e]);
     }
@@ -666,11 +668,11 @@ __global__ __launch_bounds__(BR2_T, 2) void trace_x_kernel(uint64_t *__restrict_
 #pragma unroll
     for (int p = 0; p < TRACE_X; ++p) {
       if (p == w) continue;
-      const double *srcp = xg + (((size_t)m * TRACE_X + p) * 2 + slot) * 2 * N + tid * E;
+      const double *srcp = xg + (((size_t)m * TRACE_X + p) * 2 + slot) * 2 * N + tid;
 #pragma unroll
       for (int e = 0; e < E; ++e) {
-        accA[e] += ld_sc1(srcp + e);
-        accB[e] += ld_sc1(srcp + N + e);
+        accA[e] += ld_sc1(srcp + e * T);
+        accB[e] += ld_sc1(srcp + N + e * T);
       }
     }
     // b_ntt += sigma_g(b)_ntt + B
