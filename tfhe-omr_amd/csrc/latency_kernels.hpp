@@ -332,11 +332,11 @@ __global__ __launch_bounds__(BR2L_T, 1) void br2l_kernel(const uint32_t *__restr
     }
     // exchange the partial the other group owns: group 0 sends B, group 1 sends A
 #pragma unroll
-    for (int e = 0; e < E; ++e) part[1 - g][t * E + e] = red<M>(g == 0 ? accB[e] : accA[e]);
+    for (int e = 0; e < E; ++e) part[1 - g][e * T + t] = red<M>(g == 0 ? accB[e] : accA[e]);
     __syncthreads();
     double s[E];
 #pragma unroll
-    for (int e = 0; e < E; ++e) s[e] = red<M>(red<M>(g == 0 ? accA[e] : accB[e]) + part[g][t * E + e]);
+    for (int e = 0; e < E; ++e) s[e] = red<M>(red<M>(g == 0 ? accA[e] : accB[e]) + part[g][e * T + t]);
     NTT::template inv<0>(s, X, tw, t, tb.tw2c);
 #pragma unroll
     for (int e = 0; e < E; ++e) acc[e] = canon<M>(acc[e] + s[e]);
@@ -463,12 +463,13 @@ __global__ __launch_bounds__(BR2L_T, 1) void br2x_kernel(const uint32_t *__restr
       }
       if (h + 1 < KD) cur.load(ggsw + (size_t)(h + 1) * 2 * N, N, t * E);
     }
-    // group 1's partials join group 0's (three products on a zero sum: |.| < 5.3q)
+    // group 1's partials join group 0's (three products on a zero sum: |.| < 5.3q); part[] is
+    // lane-contiguous (register e of thread t at e * 256 + t: no LDS bank conflicts)
     if (g == 1) {
 #pragma unroll
       for (int e = 0; e < E; ++e) {
-        part[0][t * E + e] = red<M>(accA[e]);
-        part[1][t * E + e] = red<M>(accB[e]);
+        part[0][e * T + t] = red<M>(accA[e]);
+        part[1][e * T + t] = red<M>(accB[e]);
       }
     }
     __syncthreads();
@@ -477,8 +478,8 @@ __global__ __launch_bounds__(BR2L_T, 1) void br2x_kernel(const uint32_t *__restr
     if (g == 0) {
 #pragma unroll
       for (int e = 0; e < E; ++e) {
-        const double sa = red<M>(red<M>(accA[e]) + part[0][t * E + e]);
-        const double sb = red<M>(red<M>(accB[e]) + part[1][t * E + e]);
+        const double sa = red<M>(red<M>(accA[e]) + part[0][e * T + t]);
+        const double sb = red<M>(red<M>(accB[e]) + part[1][e * T + t]);
         keep[e] = r == 0 ? sa : sb;
         st_sc1(xg + (((size_t)m * 2 + r) * 2 + slot) * N + e * T + t, r == 0 ? sb : sa);  // the partner's output
       }
