@@ -26,10 +26,11 @@ assert got == n, got
 arr = np.frombuffer(buf, dtype=np.uint64).astype(np.int64)
 marks = arr[: PT_SLOTS * PT_STEPS * PT_K].reshape(PT_SLOTS, PT_STEPS, PT_K)
 clk = arr[PT_SLOTS * PT_STEPS * PT_K:].reshape(PT_SLOTS, 4)
-names = {
-    "br1l": ["digits", "fwd + spectrum store", "barrier1", "mac + stores + barrier2", "outs read", "inverse", "update + barrier3"],
-    "br2x": ["stage+digits", "3 fwd + MAC + g1 partial + barrier", "g0 sum + sc1 stores + vmcnt + barrier",
-             "flag + poll + barrier", "sc1 loads + inverse", "update"],
+names = {  # phase ending at mark k (k = 1..7); br2x has no mark 2 (a mark there makes it spill)
+    "br1l": {1: "digits", 2: "fwd + spectrum store", 3: "barrier1", 4: "mac + stores + barrier2",
+             5: "outs read", 6: "inverse", 7: "update + barrier3"},
+    "br2x": {1: "stage+digits", 3: "3 fwd + MAC + g1 partial + barrier", 4: "g0 sum + sc1 stores + vmcnt + barrier",
+             5: "flag + poll + barrier", 6: "sc1 loads + inverse (g0) / barrier (g1)", 7: "update"},
 }
 for slot in range(24):
     kern = "br1l" if slot < 8 else "br2x"
@@ -39,8 +40,9 @@ for slot in range(24):
     c0, w0, c1, w1 = clk[slot]
     mhz = (c1 - c0) / ((w1 - w0) / 100.0) if w1 > w0 else float("nan")
     step = np.diff(m[:, 0]).mean() if PT_STEPS > 1 else 0
-    d = np.diff(m, axis=1).mean(axis=0)
+    present = [k for k in range(PT_K) if m[:, k].all()]  # marks this wave records
+    parts = "  ".join(f"{names[kern].get(k1, f'->{k1}')} {(m[:, k1] - m[:, k0]).mean():.0f}"
+                      for k0, k1 in zip(present, present[1:]))
     lab = f"{kern} wg{(slot - 8) // 8 if slot >= 8 else 0} wave{slot % 8}"
-    parts = "  ".join(f"{nm} {v:.0f}" for nm, v in zip(names[kern], d) if v > 0)
     print(f"{lab}: clock {mhz:.0f} MHz, step {step:.0f} cyc ({step / mhz:.2f} us) | {parts}", flush=True)
 det.close()
