@@ -176,6 +176,24 @@ omr_status omr_ctx_set_latency_threshold(omr_ctx *ctx, size_t max_messages);
  * OMR_ERR_DEVICE, clearing it; OMR_OK when every call completed correctly. Callers of the
  * device entry points use it where they would otherwise only synchronise. */
 omr_status omr_ctx_check(omr_ctx *ctx, void *hip_stream);
+/* Exactness of the FFT external products. The level-1 rotations and the throughput
+ * level-2 rotation compute each external product with FP64 FFTs and round every coefficient to the
+ * integer it equals (the reference computes it with an exact NTT: detector.rs:553-557, :623 via
+ * concrete-ntt, omr_core/Cargo.toml:38-45). With the guard on, the detect kernels run guarded
+ * variants (same output, slower) that record the largest |y - rint(y)| over every rounded
+ * coefficient: observed[0] level 1, observed[1] level 2, since context creation or the last reset.
+ * apriori[l] is the proven bound E on |computed - exact| of every such coefficient for this key
+ * (from kappa[l], the largest stored key-spectrum magnitude, computed at context creation): if
+ * E < 0.5 the rounding is exact for every input; a run with observed < 1 - E is exact (an error
+ * |e| in [0.5, E] would show a margin >= 1 - E). Any pointer may be NULL; reset != 0 zeroes the
+ * observed margins after reading them. The read synchronises the device. */
+omr_status omr_ctx_set_rounding_guard(omr_ctx *ctx, int enable);
+omr_status omr_ctx_rounding_margin(omr_ctx *ctx, double observed[2], double apriori[2],
+                                   double kappa[2], int reset);
+/* Diagnostics: `count` stored key-spectrum values (complex, re/im pairs) starting at value `first`
+ * of level 1 (BSK1, [512][8][2][512], /512) or level 2 (BSK2 limbs, [670][12][2][2][1024], /1024),
+ * in the kernels' storage order (register-major slots). */
+omr_status omr_ctx_key_spectrum(omr_ctx *ctx, int level, size_t first, size_t count, double *out);
 /* Encode workgroups fold ceil(D / max_chunks) messages each (at least 32, or 128 from D = 16,384),
  * so a call keeps at most `max_chunks` partial digests per ciphertext (32 KiB each); 0 = the
  * default 4,096. A memory knob: the digests are identical for every setting. */

@@ -139,6 +139,11 @@ pub mod ffi {
         pub fn omr_detect_with_time_info(ctx: *mut OmrCtx, clue_a: *const u16, clue_b: *const u16, d: usize,
                                          out: *mut u64, t: *mut OmrDetectTiming) -> OmrStatus;
         pub fn omr_ctx_check(ctx: *mut OmrCtx, hip_stream: *mut c_void) -> OmrStatus;
+        pub fn omr_ctx_set_rounding_guard(ctx: *mut OmrCtx, enable: c_int) -> OmrStatus;
+        pub fn omr_ctx_rounding_margin(ctx: *mut OmrCtx, observed: *mut f64, apriori: *mut f64, kappa: *mut f64,
+                                       reset: c_int) -> OmrStatus;
+        pub fn omr_ctx_key_spectrum(ctx: *mut OmrCtx, level: c_int, first: usize, count: usize,
+                                    out: *mut f64) -> OmrStatus;
         pub fn omr_encode_indices(ctx: *mut OmrCtx, pv: *const u64, d: usize, global_offset: usize,
                                   all_payloads_count: usize, seed: u64, ct: u32, out: *mut u64) -> OmrStatus;
         pub fn omr_encode_indices_device(ctx: *mut OmrCtx, d_pv: *const u64, d: usize, global_offset: usize,
@@ -455,6 +460,21 @@ impl GpuDetector {
     /// At most `max_chunks` partial digests per encode ciphertext (0 = default 4,096).
     pub fn set_encode_chunks(&self, max_chunks: usize) -> Result<(), OmrError> {
         check(unsafe { omr_ctx_set_encode_chunks(self.ctx, max_chunks) })
+    }
+
+    /// Rounding-margin guard of the FFT external products (`omr_ctx_set_rounding_guard`).
+    pub fn set_rounding_guard(&self, enable: bool) -> Result<(), OmrError> {
+        check(unsafe { omr_ctx_set_rounding_guard(self.ctx, enable as c_int) })
+    }
+
+    /// (observed margins, a priori bounds) per level (`omr_ctx_rounding_margin`): a guarded run is
+    /// exact when observed < 1 - apriori (and every run when apriori < 0.5).
+    pub fn rounding_margin(&self, reset: bool) -> Result<([f64; 2], [f64; 2]), OmrError> {
+        let (mut obs, mut apr) = ([0f64; 2], [0f64; 2]);
+        check(unsafe {
+            omr_ctx_rounding_margin(self.ctx, obs.as_mut_ptr(), apr.as_mut_ptr(), std::ptr::null_mut(), reset as c_int)
+        })?;
+        Ok((obs, apr))
     }
 
     /// Chunks of at most `max_messages` messages run the latency kernels (0 = never).

@@ -94,6 +94,59 @@ def test_shard_range_partitions():
             assert all(spans[i][0] + spans[i][1] == spans[i + 1][0] for i in range(world - 1))
 
 
+def test_launch_envs_ranks_and_mismatch():
+    """bench.py --gpus N: N rank environments when no launcher set WORLD_SIZE; none when a launcher
+    did (and it agrees) or N == 1; an error when WORLD_SIZE disagrees with N."""
+    base = {"PATH": "/usr/bin", "HSA_ENABLE_IPC_MODE_LEGACY": "0"}
+    envs = omr_dist.launch_envs(4, base, 29600)
+    assert [e["RANK"] for e in envs] == ["0", "1", "2", "3"]
+    assert all(e["LOCAL_RANK"] == e["RANK"] and e["WORLD_SIZE"] == "4" for e in envs)
+    assert all(e["MASTER_ADDR"] == "127.0.0.1" and e["MASTER_PORT"] == "29600" for e in envs)
+    assert all(e["HSA_ENABLE_IPC_MODE_LEGACY"] == "0" and e["PATH"] == "/usr/bin" for e in envs)
+    assert "RANK" not in base  # the caller's mapping is not modified
+    assert omr_dist.launch_envs(1, base, 1) is None
+    assert omr_dist.launch_envs(8, dict(base, WORLD_SIZE="8", RANK="3"), 1) is None
+    assert omr_dist.launch_envs(1, dict(base, WORLD_SIZE="1"), 1) is None
+    with pytest.raises(ValueError):
+        omr_dist.launch_envs(8, dict(base, WORLD_SIZE="1"), 1)
+    with pytest.raises(ValueError):
+        omr_dist.launch_envs(2, dict(base, WORLD_SIZE="4"), 1)
+    with pytest.raises(ValueError):
+        omr_dist.launch_envs(0, base, 1)
+
+
+def test_spawn_ranks_runs_every_rank_and_propagates_failure(tmp_path):
+    import sys
+    script = tmp_path / "child.py"
+    script.write_text(
+        "import os, sys, time\n"
+        "r = os.environ['RANK']\n"
+        "open(os.path.join(sys.argv[1], 'rank' + r), 'w').write(os.environ['WORLD_SIZE'] + ' ' + os.environ['LOCAL_RANK'])\n"
+        "if len(sys.argv) > 2 and r == sys.argv[2]:\n"
+        "    sys.exit(3)\n"
+        "if len(sys.argv) > 2:\n"
+        "    time.sleep(30)\n")
+    envs = omr_dist.launch_envs(3, dict(os.environ, WORLD_SIZE=""), 29601)
+    assert omr_dist.spawn_ranks([sys.executable, str(script), str(tmp_path)], envs, poll_s=0.05) == 0
+    assert sorted(p.name for p in tmp_path.glob("rank*")) == ["rank0", "rank1", "rank2"]
+    assert (tmp_path / "rank2").read_text() == "3 2"
+    # rank 1 fails: the others (sleeping) are terminated and its code is returned promptly
+    import time
+    t = time.perf_counter()
+    assert omr_dist.spawn_ranks([sys.executable, str(script), str(tmp_path), "1"], envs, poll_s=0.05) == 3
+    assert time.perf_counter() - t < 20
+
+
+def test_bench_rejects_gpus_world_size_mismatch():
+    """bench.py exits non-zero (before touching a GPU) when WORLD_SIZE disagrees with --gpus."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "8"],
+                       env=dict(os.environ, WORLD_SIZE="1"), capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2 and "WORLD_SIZE=1" in r.stderr and r.stdout == ""
+
+
 @pytest.mark.slow
 def test_two_rank_digest_equals_one_rank(tmp_path):
     import torch.multiprocessing as mp

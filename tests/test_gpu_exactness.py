@@ -1,0 +1,204 @@
+"""Exactness of the FFT external products at the timed geometry.
+
+The reference computes every external product with an exact modular NTT (concrete-ntt,
+omr_core/Cargo.toml:38-45; detector.rs:553-557, :623). The throughput kernels here use FP64
+FFTs and round (br1_fft.hpp, br2_fft.hpp; the latency level 1 too), so these tests prove the
+rounding exact on bench.py's own keys and clues (pack 42, key seed 7, clue seeds 1000 / 1001):
+
+- the rounding-margin guard (exactness.hpp) over one 65,536-message launch: the largest
+  |y - rint(y)| of every rounded coefficient of both levels is < 0.1, the guarded output equals
+  the production output, and the run is certified by the a priori bound (observed < 1 - E);
+- the level-1 a priori bound alone is < 0.5 (exact for every input on this key);
+- the same 65,536 clues through the latency family with the threshold raised, so level 2 runs
+  br2l_kernel's exact modular NTT (and trace_kernel): all 65,536 outputs bit-identical to the
+  throughput family's;
+- the double-double key spectra: sampled rows against a long-double restatement of the same tree
+  transform, |K^ - K| <= u |K| as the bound assumes, and kappa >= every sampled |K^|;
+- the context's hand-off buffers across mixed call sizes: detect 8 -> level-2
+  rotation of 16 -> detect 8, increasing and decreasing sizes with a raised threshold (br2x
+  accepted while trace_x is refused), each bit-exact against the throughput path, and
+  omr_ctx_check OK at the end.
+"""
+import numpy as np
+import pytest
+
+import product_lib as PL
+from product_lib import omr_amd as A
+
+pytestmark = pytest.mark.gpu
+U = 2.0 ** -53
+D_FULL = 65536
+
+
+def _device_clues(a, b, D, mask):
+    import torch
+    dev = torch.device("cuda", 0)
+    ca = torch.empty((D, A.N0), dtype=torch.int16, device=dev)
+    cb = torch.empty((D, A.CLUE_COUNT), dtype=torch.int16, device=dev)
+    na, nb = torch.empty_like(ca), torch.empty_like(cb)
+    a.gen_clues_device(1000, 0, D, ca.data_ptr(), cb.data_ptr())
+    b.gen_clues_device(1001, 0, D, na.data_ptr(), nb.data_ptr())
+    m = torch.from_numpy(mask).to(dev)[:, None]
+    return torch.where(m, ca, na).contiguous(), torch.where(m, cb, nb).contiguous()
+
+
+@pytest.fixture(scope="module")
+def full():
+    """bench.py's D = 65,536 board: production output (one 65,536-message launch) and clues."""
+    import torch
+    a, b, dk = PL.keys()
+    det = A.Detector(dk)
+    rng = np.random.default_rng(2025)
+    pert = np.sort(rng.choice(D_FULL, 50, replace=False))
+    mask = np.zeros(D_FULL, dtype=bool)
+    mask[pert] = True
+    d_ca, d_cb = _device_clues(a, b, D_FULL, mask)
+    out = torch.empty((D_FULL, 2, 2048), dtype=torch.int64, device="cuda:0")
+    det.set_batch(D_FULL)
+    torch.cuda.synchronize()
+    det.detect_batch_device(d_ca.data_ptr(), d_cb.data_ptr(), D_FULL, out.data_ptr(), None)
+    det.check()
+    yield det, d_ca, d_cb, out, mask
+    det.close()
+
+
+def test_rounding_margin_full_launch_certified(full):
+    import torch
+    det, d_ca, d_cb, want, _ = full
+    det.rounding_margin(reset=True)
+    det.set_rounding_guard(True)
+    got = torch.empty_like(want)
+    det.detect_batch_device(d_ca.data_ptr(), d_cb.data_ptr(), D_FULL, got.data_ptr(), None)
+    det.check()
+    det.set_rounding_guard(False)
+    m = det.rounding_margin(reset=True)
+    assert torch.equal(got, want), "guarded kernels changed the output"
+    obs, apr = m["observed"], m["apriori"]
+    print(f"\nrounding margin over {D_FULL} messages: level 1 {obs[0]:.3e}, level 2 {obs[1]:.3e}; "
+          f"a priori bounds {apr[0]:.3f}, {apr[1]:.3f}; kappa {m['kappa']}")
+    assert 0 < obs[0] < 0.1 and 0 < obs[1] < 0.1
+    assert apr[0] < 0.5, "level 1: exact for every input on this key"
+    for lvl in range(2):
+        assert obs[lvl] < 1 - apr[lvl], f"level {lvl + 1}: run not certified"
+
+
+def test_latency_family_exact_ntt_matches_full_launch(full):
+    """All 65,536 outputs of the throughput family (FFT level 2) equal the latency family's, whose
+    level 2 (br2l_kernel at this size: the two-CU launch does not fit) is the exact modular NTT."""
+    import torch
+    det, d_ca, d_cb, want, mask = full
+    det.set_latency_threshold(D_FULL)
+    got = torch.empty_like(want)
+    try:
+        det.detect_batch_device(d_ca.data_ptr(), d_cb.data_ptr(), D_FULL, got.data_ptr(), None)
+        det.check()
+    finally:
+        det.set_latency_threshold(64)
+    diff = (got != want).reshape(D_FULL, -1).any(dim=1)
+    bad = torch.nonzero(diff).flatten()[:8].tolist()
+    assert not bad, f"{int(diff.sum())} messages differ between the FFT and NTT level 2, e.g. {bad}"
+
+
+# ---- double-double key spectra ------------------------------------------------------------------
+def _tree_fft_ld(z, L):
+    """The natural-order tree transform of key_spectra.hpp in numpy long double (64-bit mantissa)."""
+    n = 1 << L
+    pi = np.arctan(np.longdouble(1)) * 4
+    x = z.astype(np.clongdouble).copy()
+    eps = [n]
+    for s in range(L):
+        lh = L - 1 - s
+        h = 1 << lh
+        half = np.array([e // 2 for e in eps], dtype=np.int64)
+        ang = pi * np.array(half % (4 * n), dtype=np.longdouble) / np.longdouble(2 * n)
+        w = np.cos(ang) + 1j * np.sin(ang)
+        xv = x.reshape(x.shape[0], 1 << s, 2, h)
+        v = w[None, :, None] * xv[:, :, 1, :]
+        a, b = xv[:, :, 0, :] + v, xv[:, :, 0, :] - v
+        xv[:, :, 0, :], xv[:, :, 1, :] = a, b
+        eps = [y for e in eps for y in ((e // 2) % (4 * n), (e // 2 + 2 * n) % (4 * n))]
+    return x
+
+
+def _jidx3(lane, e):  # device_fft.hpp WgFft::jidx(3, lane, e)
+    l5 = (lane >> 5) & 1
+    return ((lane & 31) << 4) | (l5 << 3) | (((e >> 1) & 1) << 2) | ((e & 1) << 1) | ((e >> 2) & 1)
+
+
+def _centred(v, q):
+    v = v.astype(np.int64) if q < 2 ** 62 else v
+    return np.where(v > (q - 1) // 2, v.astype(np.float64) - q, v.astype(np.float64))
+
+
+@pytest.mark.parametrize("level", [1, 2])
+def test_key_spectra_double_double(level):
+    import fft2_model as M2
+    _, _, dk = PL.keys()
+    det = A.Detector(dk)
+    kappa = det.rounding_margin()["kappa"][level - 1]
+    if level == 1:
+        rows = dk.bsk1.reshape(-1, 1024)
+        picks = [0, 1, 2, 3, 4095, 8191]
+        n, L = 512, 9
+        slot_index = np.array([_jidx3(s & 63, s >> 6) for s in range(n)])
+        per = 1
+    else:
+        rows = dk.bsk2.reshape(-1, 2048)
+        picks = [0, 5, 6, 11, 8000, 16079]
+        n, L = 1024, 10
+        slot_index = np.array([M2.idx(4, s & 255, s >> 8) for s in range(n)])
+        per = 2
+    worst, kmax = 0.0, 0.0
+    for p in picks:
+        got = det.key_spectrum(level, p * per * n, per * n).reshape(per, n)
+        c = _centred(rows[p], A.Q1 if level == 1 else A.Q2)
+        if level == 1:
+            limbs = [c]
+        else:
+            hi = np.rint(c / 2.0 ** 25)
+            limbs = [c - hi * 2.0 ** 25, hi]
+        for lb, cl in enumerate(limbs):
+            z = (cl[:n] + 1j * cl[n:])[None, :]
+            K = (_tree_fft_ld(z, L)[0] / n)[slot_index]
+            err = np.abs(got[lb].astype(np.clongdouble) - K)
+            assert np.all(err <= U * np.abs(K) * (1 + 2 ** -10) + 1e-18 * kappa), f"row {p} limb {lb}"
+            worst = max(worst, float(np.max(err / np.maximum(np.abs(K), 1e-300))))
+            kmax = max(kmax, float(np.max(np.abs(got[lb]))))
+    det.close()
+    assert kmax <= kappa * (1 + 1e-12)
+    print(f"\nlevel {level}: worst |K^ - K| / |K| = {worst / U:.3f} u over the sampled rows; kappa {kappa:.4e}")
+
+
+# ---- hand-off buffers across mixed call sizes --------------------------------------
+def test_handoff_buffers_mixed_sizes():
+    a, b, dk = PL.keys()
+    det = A.Detector(dk)
+    ref = A.Detector(dk)
+    ref.set_latency_threshold(0)  # throughput kernels only
+    num_cu = 256
+
+    def lwes(n, seed):
+        rng = np.random.default_rng(seed)
+        x = rng.integers(0, 4096, size=(n, A.NI + 1), dtype=np.uint32)
+        return x
+
+    def check_detect(n, seed):
+        mask = np.arange(n) % 5 == 0
+        ca, cb = PL.mixed_clues(mask, seed=seed)
+        assert np.array_equal(det.detect_batch(ca, cb), ref.detect_batch(ca, cb)), f"detect {n}"
+
+    def check_level2(n, seed):
+        x = lwes(n, seed)
+        assert np.array_equal(det.blind_rotate_level2(x), ref.blind_rotate_level2(x)), f"level 2 {n}"
+
+    check_detect(8, 1)
+    check_level2(16, 2)   # grows the two-CU slots only
+    check_detect(8, 3)    # the trace slots of the first call must still be valid
+    det.set_latency_threshold(num_cu)  # n in (0.4, 0.5] x num_cu: br2x accepted, trace_x refused
+    for n, s in ((110, 4), (128, 5), (40, 6), (8, 7)):
+        check_detect(n, s)
+    check_level2(100, 8)
+    check_detect(8, 9)
+    det.check()
+    det.close()
+    ref.close()

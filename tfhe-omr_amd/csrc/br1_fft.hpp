@@ -13,6 +13,7 @@
 #pragma once
 
 #include "device_fft.hpp"
+#include "exactness.hpp"
 #include "kernels.hpp"
 
 namespace omr {
@@ -35,9 +36,13 @@ struct Lvl1Int {
   // as an int. The quotient is rint(y / q) and r = y - kq keeps the fraction; adding 1.5 * 2^52
   // rounds r to the nearest integer in the low mantissa bits, which are its two's complement
   // (|round(r)| <= H + 1): one FP64 add instead of rint + conversion.
-  __device__ static __forceinline__ int round_red(double y) {
+  // With a RoundGuard, |r - round(r)| = |y - rint(y)| (r = y - kq is exact) is recorded.
+  template <bool G = false>
+  __device__ static __forceinline__ int round_red(double y, RoundGuard<G> *rg = nullptr) {
     const double r = __fma_rn(-rint(y * (1.0 / 134215681.0)), 134215681.0, y);
-    return (int)(uint32_t)__builtin_bit_cast(uint64_t, r + 6755399441055744.0);
+    const double s = r + 6755399441055744.0;
+    if constexpr (G) rg->note(r, s - 6755399441055744.0);
+    return (int)(uint32_t)__builtin_bit_cast(uint64_t, s);
   }
   // NonPowOf2ApproxSignedBasis (logB 5, d 4, drop 7) on a canonical residue: y = floor((v + 2^6)
   // / 2^7) has balanced base-32 digits d_k in [-16, 15] (k < 3) and an unbounded top digit; in
@@ -149,10 +154,11 @@ __device__ __forceinline__ void vm_wait_all() {  // s_waitcnt vmcnt(0)
 // One CMUX step with LDS-staged key rows. q0 = first global row of this step; rows q0..q0+7 are
 // consumed, the next step's first row is prefetched on the way. xch: the wave's exchange buffer
 // (Fft512::BUF).
+template <bool G>
 __device__ __forceinline__ void br1f_step_lds(uint32_t (&ac)[2][16], double2 *xch, const double2 *tws, int a,
                                               const double2 *__restrict__ bskf, int q0, int qtotal,
                                               double2 *kbuf, int lane, int wave,
-                                              const double2 *__restrict__ gtw) {
+                                              const double2 *__restrict__ gtw, RoundGuard<G> &rg) {
   using F = Fft512;
   uint32_t pk[2][16];
   br1f_digits(ac, reinterpret_cast<uint32_t *>(xch), a, lane, pk);
@@ -197,18 +203,20 @@ __device__ __forceinline__ void br1f_step_lds(uint32_t (&ac)[2][16], double2 *xc
   for (int o = 0; o < 2; ++o)
 #pragma unroll
     for (int i = 0; i < 16; ++i)
-      ac[o][i] = Lvl1Off::add(ac[o][i], Lvl1Int::round_red(i < 8 ? outr[o][i] : outi[o][i - 8]));
+      ac[o][i] = Lvl1Off::add(ac[o][i], Lvl1Int::round_red<G>(i < 8 ? outr[o][i] : outi[o][i - 8], &rg));
 }
 
 // Level-1 blind rotations: BR1F_WPG waves per workgroup, one rotation per wave; rotation
 // g = wg * BR1F_WPG + wave: clue g % 7 of message g / 7 (lwe_a == nullptr) or LWE g; nrot bounds
 // g. The transforms are wave-private (wave-level LDS sync); the waves run the CMUX steps in
 // lockstep, sharing each key row staged in LDS and one twiddle table.
-__global__ __launch_bounds__(64 * BR1F_WPG, 2) void br1f_kernel(
+// G: the rounding-margin guard (exactness.hpp) publishes the largest |y - rint(y)| to *margin.
+template <bool G>
+__device__ __forceinline__ void br1f_body(
     const uint16_t *__restrict__ clue_a, const uint16_t *__restrict__ clue_b,
     const uint16_t *__restrict__ lwe_a, const uint16_t *__restrict__ lwe_b,
     const double2 *__restrict__ bskf, DeviceTables tb, uint32_t *__restrict__ ext,
-    uint64_t *__restrict__ rlwe_out, int mode, size_t nrot) {
+    uint64_t *__restrict__ rlwe_out, int mode, size_t nrot, unsigned long long *margin) {
   constexpr int NF = Fft512::N, W = BR1F_WPG;
   static_assert(16 % W == 0, "LDS key staging: W divides the row's 16 one-KiB pieces");
   __shared__ double2 xch_all[W][Fft512::BUF];
@@ -245,11 +253,13 @@ __global__ __launch_bounds__(64 * BR1F_WPG, 2) void br1f_kernel(
   // every step runs (a = 0 gives zero digits and leaves ACC unchanged) so the waves share the
   // staged key rows; row 0 is issued before the loop
   krow_issue(bskf, kbuf, lane, wave);
+  RoundGuard<G> rg;
 #pragma unroll 1
   for (int i = 0; i < N0; ++i) {
     const int a = __builtin_amdgcn_readfirstlane(la[i]);
-    br1f_step_lds(ac, xch, tws, a, bskf, i * 2 * D1, N0 * 2 * D1, kbuf, lane, wave, tb.fft1);
+    br1f_step_lds<G>(ac, xch, tws, a, bskf, i * 2 * D1, N0 * 2 * D1, kbuf, lane, wave, tb.fft1, rg);
   }
+  rg.publish(margin);
   __syncthreads();
   if (g >= nrot) return;
   if (mode == 0) {  // extract_lwe_locally (coefficient 0), detector.rs:561
@@ -274,29 +284,19 @@ __global__ __launch_bounds__(64 * BR1F_WPG, 2) void br1f_kernel(
   }
 }
 
-// Coefficient-domain canonical u32 key polynomials -> FFT domain / 512, transform-index order.
-__global__ __launch_bounds__(64) void key_to_fft1_kernel(const uint32_t *__restrict__ in,
-                                                         double2 *__restrict__ out, size_t npoly,
-                                                         const double2 *__restrict__ tw) {
-  using F = Fft512;
-  __shared__ double2 xch[F::BUF];
-  __shared__ double2 tws[F::N];
-  const int lane = threadIdx.x;
-  const size_t poly = blockIdx.x;
-  if (poly >= npoly) return;
-  const uint32_t *src = in + poly * N1;
-  double xr[8], xi[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    tws[lane + 64 * e] = tw[lane + 64 * e];
-    xr[e] = from_u64<Mod<1>>(src[lane + 64 * e]);
-    xi[e] = from_u64<Mod<1>>(src[lane + 64 * e + 512]);
-  }
-  __syncthreads();
-  F::fwd(xr, xi, xch, tws, lane);
-  double2 *dst = out + poly * F::N;
-#pragma unroll
-  for (int e = 0; e < 8; ++e) dst[key1_pos(lane, e)] = make_double2(xr[e] * (1.0 / 512), xi[e] * (1.0 / 512));
+__global__ __launch_bounds__(64 * BR1F_WPG, 2) void br1f_kernel(
+    const uint16_t *__restrict__ clue_a, const uint16_t *__restrict__ clue_b,
+    const uint16_t *__restrict__ lwe_a, const uint16_t *__restrict__ lwe_b,
+    const double2 *__restrict__ bskf, DeviceTables tb, uint32_t *__restrict__ ext,
+    uint64_t *__restrict__ rlwe_out, int mode, size_t nrot) {
+  br1f_body<false>(clue_a, clue_b, lwe_a, lwe_b, bskf, tb, ext, rlwe_out, mode, nrot, nullptr);
+}
+__global__ __launch_bounds__(64 * BR1F_WPG, 2) void br1f_guard_kernel(
+    const uint16_t *__restrict__ clue_a, const uint16_t *__restrict__ clue_b,
+    const uint16_t *__restrict__ lwe_a, const uint16_t *__restrict__ lwe_b,
+    const double2 *__restrict__ bskf, DeviceTables tb, uint32_t *__restrict__ ext,
+    uint64_t *__restrict__ rlwe_out, int mode, size_t nrot, unsigned long long *margin) {
+  br1f_body<true>(clue_a, clue_b, lwe_a, lwe_b, bskf, tb, ext, rlwe_out, mode, nrot, margin);
 }
 
 // Test entry (omr_fft1_mul): out = a * k mod (X^1024 + 1, q1) through the level-1 FFT path,

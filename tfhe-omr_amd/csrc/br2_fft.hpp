@@ -254,43 +254,9 @@ constexpr double LIMB = 33554432.0;  // 2^25: key = lo + 2^25 hi
 // (profiles/r03q/key_layout_ab.log).
 __device__ __forceinline__ int key_pos(int t, int e) { return e * Fft1024::T + t; }
 
-// BSK2 rows (canonical u64 [670][12][2][2048]) -> FFT-domain limbs, x 1/1024:
-// out double2 [670][12][2 out][2 limb][1024], point 4 t + e (Fft1024's P4 layout) at key_pos(t, e).
-__global__ __launch_bounds__(256) void key_to_fft2_kernel(const uint64_t *__restrict__ in, double2 *__restrict__ out,
-                                                          size_t npoly, const double2 *__restrict__ twg) {
-  using F = Fft1024;
-  using M = Mod<2>;
-  __shared__ double2 tws[F::TW_LEN];
-  __shared__ double2 X[F::n], W[F::n];
-  const int t = threadIdx.x;
-  const size_t poly = blockIdx.x;
-  if (poly >= npoly) return;
-  F::load_twiddles(tws, twg, t);
-  const uint64_t *src = in + poly * N2;
-  double lr[2][F::E], li[2][F::E];  // [limb][point]
-#pragma unroll
-  for (int e = 0; e < F::E; ++e) {
-    const int j = F::idx(0, t, e);
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const double k = from_u64<M>(src[j + h * F::n]);
-      const double hi = rint(k * (1.0 / LIMB));
-      const double lo = __fma_rn(-hi, LIMB, k);
-      (h ? li : lr)[0][e] = lo;
-      (h ? li : lr)[1][e] = hi;
-    }
-  }
-  __syncthreads();
-#pragma unroll
-  for (int l = 0; l < 2; ++l) {
-    F::fwd(lr[l], li[l], X, W, tws, t);
-    __syncthreads();  // X is reused by the next limb's exchange
-    double2 *dst = out + (poly * 2 + l) * F::n;
-#pragma unroll
-    for (int e = 0; e < F::E; ++e)
-      dst[key_pos(t, e)] = make_double2(lr[l][e] * (1.0 / F::n), li[l][e] * (1.0 / F::n));
-  }
-}
+// BSK2 rows (canonical u64 [670][12][2][2048]) -> FFT-domain limbs, x 1/1024, as double2
+// [670][12][2 out][2 limb][1024], point idx(4, t, e) at key_pos(t, e): key_spectrum_dd_kernel<2>
+// (key_spectra.hpp), in double-double.
 
 // Level-2 blind rotation (BlindRotationKey::blind_rotate, detector.rs:623) on the exact FFT: one
 // 256-thread workgroup per message, ACC in registers (P0 layout: coefficients j and j + 1024 of the
@@ -303,10 +269,11 @@ __global__ __launch_bounds__(256) void key_to_fft2_kernel(const uint64_t *__rest
 // X0, inverses X1 X0 X1 X0), so no use needs a trailing barrier (the rule of cmux_step3).
 // mode 0: then hom_trace (detector.rs:626-639) with the accumulator re-laid out for the trace's
 // NTTs, output the NttRlweCiphertext; mode 1: the coefficient-domain rotation (stage tests).
-__global__ __launch_bounds__(256, 2) void br2f_kernel(const uint32_t *__restrict__ lwe_int,
-                                                      const double2 *__restrict__ bskf,
-                                                      const double2 *__restrict__ twg, const double *__restrict__ tk,
-                                                      DeviceTables tb, uint64_t *__restrict__ out, int mode) {
+template <bool G>
+__device__ __forceinline__ void br2f_body(const uint32_t *__restrict__ lwe_int, const double2 *__restrict__ bskf,
+                                          const double2 *__restrict__ twg, const double *__restrict__ tk,
+                                          DeviceTables tb, uint64_t *__restrict__ out, int mode,
+                                          unsigned long long *margin) {
   using F = Fft1024;
   using M = Mod<2>;
   using DG = Digits2;
@@ -346,6 +313,7 @@ __global__ __launch_bounds__(256, 2) void br2f_kernel(const uint32_t *__restrict
       for (int e = 0; e < E; ++e) k[l][e] = row[(o * 2 + l) * F::n + key_pos(t, e)];
   };
   constexpr size_t ROW = 4 * F::n;  // double2 per GGSW row
+  RoundGuard<G> rg;
 #pragma unroll 1
   for (int i = 0; i < NI; ++i) {
     const int a = (int)__builtin_amdgcn_readfirstlane(lwe[i]) & (2 * NN - 1);
@@ -428,12 +396,16 @@ __global__ __launch_bounds__(256, 2) void br2f_kernel(const uint32_t *__restrict
       for (int e = 0; e < E; ++e)
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-          const double lo = rint(h ? si[o][0][e] : sr[o][0][e]);
-          const double hi = rint(h ? si[o][1][e] : sr[o][1][e]) * LIMB;  // exact (|P_hi| < 2^45)
+          const double ylo = h ? si[o][0][e] : sr[o][0][e], yhi = h ? si[o][1][e] : sr[o][1][e];
+          const double lo = rint(ylo), hr = rint(yhi);
+          rg.note(ylo, lo);
+          rg.note(yhi, hr);
+          const double hi = hr * LIMB;  // exact (|P_hi| < 2^45)
           ac[o][h][e] = canon<M>(ac[o][h][e] + red<M>(hi) + lo);
         }
     }
   }
+  rg.publish(margin);
   uint64_t *o = out + (size_t)blockIdx.x * 2 * NN;
   if (mode == 1) {
 #pragma unroll
@@ -469,6 +441,20 @@ __global__ __launch_bounds__(256, 2) void br2f_kernel(const uint32_t *__restrict
   }
   __syncthreads();
   hom_trace_store(acc0, acc1, xch, tw, xch + 2 * NN, tk, tb, o, t);
+}
+
+__global__ __launch_bounds__(256, 2) void br2f_kernel(const uint32_t *__restrict__ lwe_int,
+                                                      const double2 *__restrict__ bskf,
+                                                      const double2 *__restrict__ twg, const double *__restrict__ tk,
+                                                      DeviceTables tb, uint64_t *__restrict__ out, int mode) {
+  br2f_body<false>(lwe_int, bskf, twg, tk, tb, out, mode, nullptr);
+}
+__global__ __launch_bounds__(256, 2) void br2f_guard_kernel(const uint32_t *__restrict__ lwe_int,
+                                                            const double2 *__restrict__ bskf,
+                                                            const double2 *__restrict__ twg, const double *__restrict__ tk,
+                                                            DeviceTables tb, uint64_t *__restrict__ out, int mode,
+                                                            unsigned long long *margin) {
+  br2f_body<true>(lwe_int, bskf, twg, tk, tb, out, mode, margin);
 }
 
 }  // namespace omr

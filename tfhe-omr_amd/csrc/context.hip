@@ -16,6 +16,7 @@
 #include "br2_fft.hpp"
 #include "detect_kernels.hpp"
 #include "encode_kernels.hpp"
+#include "key_spectra.hpp"
 #include "latency_kernels.hpp"
 
 using namespace omr;
@@ -150,6 +151,73 @@ std::vector<double2> fft2_twiddles() {
   return tw;
 }
 
+// ---- exact twiddles of the double-double key transforms (key_spectra.hpp) ----
+// exp(i pi h / 2n) in double-double: quadrant and complement reduction on the integer h, then
+// Taylor series of sin / cos on [0, pi/4] (terms below 2^-110 dropped): accurate to a few 2^-104.
+DD dd_div_d(DD a, double b) {
+  const double q1 = a.hi / b, p = q1 * b, pe = std::fma(q1, b, -p);
+  return dd_quick(q1, ((a.hi - p) - pe + a.lo) / b);
+}
+void dd_sincos(DD x, DD &sn, DD &cs) {  // 0 <= x <= pi / 4
+  const DD x2 = dd_mul(x, x);
+  DD ts = x, tc = {1.0, 0.0};
+  sn = x;
+  cs = tc;
+  for (int k = 1; k < 20; ++k) {
+    ts = dd_div_d(dd_mul(ts, x2), (double)((2 * k) * (2 * k + 1)));
+    tc = dd_div_d(dd_mul(tc, x2), (double)((2 * k - 1) * (2 * k)));
+    sn = dd_add(sn, k & 1 ? dd_neg(ts) : ts);
+    cs = dd_add(cs, k & 1 ? dd_neg(tc) : tc);
+  }
+}
+CDD dd_expi(long h, long n) {
+  const DD PI = {3.141592653589793116, 1.2246467991473532e-16};
+  const long r = ((h % (4 * n)) + 4 * n) % (4 * n);  // angle pi r / 2n, period 4n
+  const long quad = r / n, rho = r % n;               // quad * pi/2 + pi rho / 2n
+  const bool comp = 2 * rho > n;                      // beyond pi/4: use the complement
+  const long m = comp ? n - rho : rho;
+  DD sn, cs;
+  dd_sincos(dd_mul(PI, DD{(double)m / (2.0 * (double)n), 0.0}), sn, cs);
+  DD c = comp ? sn : cs, s = comp ? cs : sn;  // cos, sin of pi rho / 2n
+  for (long q = 0; q < quad; ++q) {             // rotate by pi/2: (c, s) -> (-s, c)
+    const DD t = c;
+    c = dd_neg(s);
+    s = t;
+  }
+  return {c, s};
+}
+// tree twiddles W(s, i) = w^(eps(s, i) / 2), stage s node i at (1 << s) - 1 + i (dd_tree_fft)
+std::vector<CDD> dd_tree_twiddles(int L) {
+  const long n = 1L << L;
+  std::vector<CDD> tw;
+  std::vector<long> eps{n};
+  for (int s = 0; s < L; ++s) {
+    std::vector<long> next;
+    for (long e : eps) {
+      tw.push_back(dd_expi(e / 2, n));
+      next.push_back((e / 2) % (4 * n));
+      next.push_back((e / 2 + 2 * n) % (4 * n));
+    }
+    eps.swap(next);
+  }
+  return tw;
+}
+
+// A priori bound on |computed - exact| of every rounded coefficient of one external product
+// (DESIGN.md §3): E = n R D kappa (2 delta_f + sqrt(2) (R + 1) u + u (1 + 2^-40)), with n complex
+// points, R GGSW rows, D = sqrt(2n) d_max the 2-norm bound of a digit polynomial, delta_f = 26u the
+// forward / inverse transform's relative 2-norm error (5u per radix-4 pass, 8u per radix-8, 4u
+// per radix-2, rounded up), the sequential fma accumulation over R rows, and the double-double
+// keys' |K^ - K| <= u |K|.
+double apriori_bound(int level, double kappa) {
+  const double u = 0x1p-53;
+  const int n = level == 1 ? 512 : 1024, R = level == 1 ? 2 * D1 : 2 * D2;
+  const double dmax = level == 1 ? 16.0 : 64.0;
+  const double D = std::sqrt(2.0 * n) * dmax;
+  const double coef = 2 * 26 * u + std::sqrt(2.0) * (R + 1) * u + u * (1 + 0x1p-40);
+  return (double)n * R * D * kappa * (1 + 0x1p-40) * coef;
+}
+
 }  // namespace
 
 #ifndef OMR_DEFAULT_LATENCY_MAX
@@ -189,6 +257,12 @@ struct omr_ctx {
   size_t t_cap = 0;
   int num_cu = 0;
   bool coop = false;  // hipDeviceAttributeCooperativeLaunch
+  // rounding-margin guard (exactness.hpp): guarded kernel variants when on; margin[0] level 1,
+  // margin[1] level 2 (bits of the largest |y - rint(y)|); kappa: largest stored key spectrum
+  // magnitude per level; apriori: the bound it gives (apriori_bound)
+  bool guard = false;
+  unsigned long long *margin = nullptr;
+  double kappa[2] = {0.0, 0.0}, apriori[2] = {0.0, 0.0};
   // host-API staging
   uint16_t *s_clue_a = nullptr, *s_clue_b = nullptr;
   uint64_t *s_out = nullptr;
@@ -225,6 +299,13 @@ void dev_free(T *&p) {
   if (p) (void)hipFree((void *)p);
   p = nullptr;
 }
+
+// Scoped device allocation (freed on every return path).
+template <typename T>
+struct DevBufHost {
+  T *p = nullptr;
+  ~DevBufHost() { dev_free(p); }
+};
 
 // Scratch reuse across streams (see omr_ctx::scratch_free). Callers hold c->mu.
 omr_status scratch_acquire(omr_ctx *c, hipStream_t st) {
@@ -328,34 +409,25 @@ omr_status convert_keys_cmux(const uint64_t *host, size_t npoly, double *dev, do
   return OMR_OK;
 }
 
-omr_status convert_keys_fft2(const uint64_t *host, size_t npoly, double2 *dev, const double2 *tw, hipStream_t st) {
+// BSK1 / BSK2 -> FFT-domain key spectra in double-double, rounded once (key_spectra.hpp).
+template <int LEVEL, typename IN>
+omr_status convert_keys_dd(const IN *host, size_t npoly, double2 *dev, hipStream_t st) {
+  constexpr int N = LEVEL == 1 ? N1 : N2;
+  const auto twv = dd_tree_twiddles(LEVEL == 1 ? 9 : 10);
+  DevBufHost<CDD> tw;
+  HIP_TRY(hipMalloc(&tw.p, twv.size() * sizeof(CDD)));
+  HIP_TRY(hipMemcpy(tw.p, twv.data(), twv.size() * sizeof(CDD), hipMemcpyHostToDevice));
   const size_t chunk = 4096;  // polynomials per upload
-  uint64_t *tmp = nullptr;
-  HIP_TRY(hipMalloc(&tmp, chunk * N2 * sizeof(uint64_t)));
+  DevBufHost<IN> tmp;
+  HIP_TRY(hipMalloc(&tmp.p, chunk * N * sizeof(IN)));
   for (size_t p0 = 0; p0 < npoly; p0 += chunk) {
     const size_t n = std::min(chunk, npoly - p0);
-    HIP_TRY(hipMemcpyAsync(tmp, host + p0 * N2, n * N2 * sizeof(uint64_t), hipMemcpyDefault, st));
-    key_to_fft2_kernel<<<n, Fft1024::T, 0, st>>>(tmp, dev + p0 * 2 * Fft1024::n, n, tw);
+    HIP_TRY(hipMemcpyAsync(tmp.p, host + p0 * N, n * N * sizeof(IN), hipMemcpyDefault, st));
+    key_spectrum_dd_kernel<LEVEL><<<(unsigned)(n * (LEVEL == 1 ? 1 : 2)), KDD_T, 0, st>>>(
+        tmp.p, dev + p0 * (LEVEL == 1 ? Fft512::N : 2 * Fft1024::n), n, tw.p);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(st));
   }
-  dev_free(tmp);
-  return OMR_OK;
-}
-
-omr_status convert_keys_fft1(const uint32_t *host, size_t npoly, double2 *dev, const double2 *tw,
-                             hipStream_t st) {
-  const size_t chunk = 4096;
-  uint32_t *tmp = nullptr;
-  HIP_TRY(hipMalloc(&tmp, chunk * N1 * sizeof(uint32_t)));
-  for (size_t p0 = 0; p0 < npoly; p0 += chunk) {
-    const size_t n = std::min(chunk, npoly - p0);
-    HIP_TRY(hipMemcpyAsync(tmp, host + p0 * N1, n * N1 * sizeof(uint32_t), hipMemcpyDefault, st));
-    key_to_fft1_kernel<<<n, 64, 0, st>>>(tmp, dev + p0 * Fft512::N, n, tw);
-    HIP_TRY(hipGetLastError());
-    HIP_TRY(hipStreamSynchronize(st));
-  }
-  dev_free(tmp);
   return OMR_OK;
 }
 
@@ -396,11 +468,18 @@ omr_status launch_ks(omr_ctx *c, int B, uint32_t *out, hipStream_t st) {
 omr_status launch_br1(omr_ctx *c, size_t n, const uint16_t *ca, const uint16_t *cb,
                       const uint16_t *la, const uint16_t *lb, uint32_t *ext, uint64_t *rlwe, int mode,
                       hipStream_t st, size_t msgs) {
-  if (latency_path(c, msgs))
-    br1l_kernel<<<(unsigned)n, 64 * BR1L_WAVES, 0, st>>>(ca, cb, la, lb, c->bsk1l, c->tb, ext, rlwe, mode);
-  else
-    br1f_kernel<<<(unsigned)((n + BR1F_WPG - 1) / BR1F_WPG), 64 * BR1F_WPG, 0, st>>>(
-        ca, cb, la, lb, c->bsk1f, c->tb, ext, rlwe, mode, n);
+  const unsigned g1 = (unsigned)((n + BR1F_WPG - 1) / BR1F_WPG);
+  if (latency_path(c, msgs)) {
+    if (c->guard)
+      br1l_guard_kernel<<<(unsigned)n, 64 * BR1L_WAVES, 0, st>>>(ca, cb, la, lb, c->bsk1l, c->tb, ext, rlwe, mode,
+                                                                  c->margin);
+    else
+      br1l_kernel<<<(unsigned)n, 64 * BR1L_WAVES, 0, st>>>(ca, cb, la, lb, c->bsk1l, c->tb, ext, rlwe, mode);
+  } else if (c->guard) {
+    br1f_guard_kernel<<<g1, 64 * BR1F_WPG, 0, st>>>(ca, cb, la, lb, c->bsk1f, c->tb, ext, rlwe, mode, n, c->margin);
+  } else {
+    br1f_kernel<<<g1, 64 * BR1F_WPG, 0, st>>>(ca, cb, la, lb, c->bsk1f, c->tb, ext, rlwe, mode, n);
+  }
   HIP_TRY(hipGetLastError());
   return OMR_OK;
 }
@@ -415,8 +494,6 @@ omr_status launch_br2x(omr_ctx *c, size_t n, const uint32_t *lwe_int, uint64_t *
     omr_status s;
     if ((s = scratch_idle(c)) != OMR_OK) return s;
     dev_free(c->x_slots);
-  dev_free(c->t_slots);
-  dev_free(c->t_flags);
     dev_free(c->x_flags);
     c->x_cap = 0;
     HIP_TRY(hipMalloc(&c->x_slots, n * 4 * N2 * sizeof(double)));
@@ -501,8 +578,12 @@ omr_status launch_br2(omr_ctx *c, size_t n, const uint32_t *lwe_int, uint64_t *o
     if (!two_cu) br2l_kernel<<<(unsigned)n, BR2L_T, 0, st>>>(lwe_int, c->bsk2, c->tb, out);
     split_trace = true;
   } else {
-    br2f_kernel<<<(unsigned)n, Fft1024::T, 0, st>>>(lwe_int, c->bsk2f, c->fft2, c->tk, c->tb, out,
-                                                    split_trace && mode == 0 ? 1 : mode);
+    const int m = split_trace && mode == 0 ? 1 : mode;
+    if (c->guard)
+      br2f_guard_kernel<<<(unsigned)n, Fft1024::T, 0, st>>>(lwe_int, c->bsk2f, c->fft2, c->tk, c->tb, out, m,
+                                                            c->margin + 1);
+    else
+      br2f_kernel<<<(unsigned)n, Fft1024::T, 0, st>>>(lwe_int, c->bsk2f, c->fft2, c->tk, c->tb, out, m);
   }
   HIP_TRY(hipGetLastError());
   if (mid) HIP_TRY(hipEventRecord(mid, st));
@@ -622,14 +703,30 @@ extern "C" omr_status omr_ctx_create(const omr_detection_key_view *key, int devi
     return fail(set_error(OMR_ERR_OUT_OF_MEMORY, "omr_ctx_create: key buffers"));
   const double ninv2 = centred(h_powmod(N2, Q2 - 2, Q2), Q2);
   omr_status st;
-  if ((st = convert_keys_fft1(key->bsk1, BSK1_ELEMS / N1, c->bsk1f, c->fft1, c->stream)) != OMR_OK)
-    return fail(st);
+  if ((st = convert_keys_dd<1>(key->bsk1, BSK1_ELEMS / N1, c->bsk1f, c->stream)) != OMR_OK) return fail(st);
   bsk1_latency_layout_kernel<<<(unsigned)(BSK1_ELEMS / 2 / 256), 256, 0, c->stream>>>(c->bsk1f, c->bsk1l,
                                                                                      BSK1_ELEMS / 2);
   if (hipGetLastError() != hipSuccess) return fail(set_error(OMR_ERR_DEVICE, "omr_ctx_create: BSK1 layout"));
   if ((st = convert_keys_cmux(key->bsk2, BSK2_ELEMS / N2, c->bsk2, ninv2, c->tb.tw2c, c->stream)) != OMR_OK)
     return fail(st);
-  if ((st = convert_keys_fft2(key->bsk2, BSK2_ELEMS / N2, c->bsk2f, c->fft2, c->stream)) != OMR_OK) return fail(st);
+  if ((st = convert_keys_dd<2>(key->bsk2, BSK2_ELEMS / N2, c->bsk2f, c->stream)) != OMR_OK) return fail(st);
+  {  // kappa per level (the a priori bound's key constant) and the guard's margin words
+    if (hipMalloc(&c->margin, 4 * sizeof(unsigned long long)) != hipSuccess)
+      return fail(set_error(OMR_ERR_OUT_OF_MEMORY, "omr_ctx_create: margin words"));
+    const bool ok = hipMemsetAsync(c->margin, 0, 4 * sizeof(unsigned long long), c->stream) == hipSuccess;
+    if (ok) {
+      max_abs_kernel<<<1024, 256, 0, c->stream>>>(c->bsk1f, BSK1_ELEMS / 2, c->margin + 2);
+      max_abs_kernel<<<2048, 256, 0, c->stream>>>(c->bsk2f, BSK2_ELEMS, c->margin + 3);
+    }
+    unsigned long long w[2] = {0, 0};
+    if (!ok || hipGetLastError() != hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess ||
+        hipMemcpy(w, c->margin + 2, sizeof(w), hipMemcpyDeviceToHost) != hipSuccess)
+      return fail(set_error(OMR_ERR_DEVICE, "omr_ctx_create: key spectrum maxima"));
+    for (int l = 0; l < 2; ++l) {
+      c->kappa[l] = __builtin_bit_cast(double, w[l]);
+      c->apriori[l] = apriori_bound(l + 1, c->kappa[l]);
+    }
+  }
   if ((st = convert_keys<2, uint64_t, double>(key->trace_key, TK_ELEMS / N2, c->tk, 1.0, c->tb.tw2,
                                               c->stream)) != OMR_OK)
     return fail(st);
@@ -674,6 +771,9 @@ extern "C" void omr_ctx_destroy(omr_ctx *c) {
   dev_free(c->ks_part);
   dev_free(c->x_slots);
   dev_free(c->x_flags);
+  dev_free(c->t_slots);
+  dev_free(c->t_flags);
+  dev_free(c->margin);
   dev_free(c->x_err);
   if (c->x_err_host) (void)hipHostFree(c->x_err_host);
   for (auto e : c->events) (void)hipEventDestroy(e);
@@ -713,6 +813,40 @@ extern "C" omr_status omr_ctx_enable_timing(omr_ctx *c, int mode) {
   if (!c || mode < 0 || mode > 2) return set_error(OMR_ERR_INVALID_ARGUMENT, "omr_ctx_enable_timing: bad argument");
   std::lock_guard<std::mutex> lk(c->mu);
   c->timing = mode;
+  return OMR_OK;
+}
+
+extern "C" omr_status omr_ctx_set_rounding_guard(omr_ctx *c, int enable) {
+  if (!c) return set_error(OMR_ERR_INVALID_ARGUMENT, "omr_ctx_set_rounding_guard: NULL ctx");
+  std::lock_guard<std::mutex> lk(c->mu);
+  c->guard = enable != 0;
+  return OMR_OK;
+}
+
+extern "C" omr_status omr_ctx_rounding_margin(omr_ctx *c, double observed[2], double apriori[2], double kappa[2],
+                                              int reset) {
+  if (!c) return set_error(OMR_ERR_INVALID_ARGUMENT, "omr_ctx_rounding_margin: NULL ctx");
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipDeviceSynchronize());  // every guarded launch on any stream has published
+  unsigned long long w[2];
+  HIP_TRY(hipMemcpy(w, c->margin, sizeof(w), hipMemcpyDeviceToHost));
+  for (int l = 0; l < 2; ++l) {
+    if (observed) observed[l] = __builtin_bit_cast(double, w[l]);
+    if (apriori) apriori[l] = c->apriori[l];
+    if (kappa) kappa[l] = c->kappa[l];
+  }
+  if (reset) HIP_TRY(hipMemset(c->margin, 0, 2 * sizeof(unsigned long long)));
+  return OMR_OK;
+}
+
+extern "C" omr_status omr_ctx_key_spectrum(omr_ctx *c, int level, size_t first, size_t count, double *out) {
+  const size_t total = level == 1 ? BSK1_ELEMS / 2 : BSK2_ELEMS;  // double2 values
+  if (!c || !out || (level != 1 && level != 2) || first > total || count > total - first)
+    return set_error(OMR_ERR_INVALID_ARGUMENT, "omr_ctx_key_spectrum: bad argument");
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipMemcpy(out, (level == 1 ? c->bsk1f : c->bsk2f) + first, count * sizeof(double2), hipMemcpyDeviceToHost));
   return OMR_OK;
 }
 

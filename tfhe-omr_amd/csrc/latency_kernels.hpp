@@ -73,11 +73,12 @@ __global__ __launch_bounds__(256) void bsk1_latency_layout_kernel(const double2 
   out[idx] = in[((i * 8 + r) * 2 + o) * 512 + key1_pos(lane, e)];
 }
 
-__global__ __launch_bounds__(64 * BR1L_WAVES, 1) void br1l_kernel(
+template <bool G>
+__device__ __forceinline__ void br1l_body(
     const uint16_t *__restrict__ clue_a, const uint16_t *__restrict__ clue_b,
     const uint16_t *__restrict__ lwe_a, const uint16_t *__restrict__ lwe_b,
     const double2 *__restrict__ bskl, DeviceTables tb, uint32_t *__restrict__ ext_out,
-    uint64_t *__restrict__ rlwe_out, int mode) {
+    uint64_t *__restrict__ rlwe_out, int mode, unsigned long long *margin) {
   using F = Fft512;
   constexpr int NF = F::N, W = BR1L_WAVES;
   static_assert(W == 8 && NF == 8 * 64, "one wave per GGSW row and per register slot");
@@ -134,6 +135,7 @@ __global__ __launch_bounds__(64 * BR1L_WAVES, 1) void br1l_kernel(
   };
   const int pslot = __builtin_amdgcn_readfirstlane(blockIdx.x == 0 ? wave : -1);
   int hs = 0;
+  RoundGuard<G> rg;  // waves 0 / 1 round the inverses
   (void)pslot;
   (void)hs;
   // one CMUX step at executed step i with its key slice kk (kko: the other slice buffer; inext,
@@ -197,7 +199,8 @@ __global__ __launch_bounds__(64 * BR1L_WAVES, 1) void br1l_kernel(
       OMR_PHASE(pslot, hs, 6);
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
-        const double v = rint(q < 8 ? sr[0][q] : si[0][q - 8]);  // exact (< 2^43)
+        const double y = q < 8 ? sr[0][q] : si[0][q - 8], v = rint(y);  // exact (< 2^43)
+        rg.note(y, v);
         ac[q] = Lvl1Int::canon(ac[q] + (int)red<Mod<1>>(v));
         ext[wave][acc_coef(lane, q)] = ac[q];
         ext[wave][N1 + acc_coef(lane, q)] = -ac[q];
@@ -224,6 +227,7 @@ __global__ __launch_bounds__(64 * BR1L_WAVES, 1) void br1l_kernel(
     i1 = i3;
   }
   OMR_PHASE_CLOCK(pslot, 1);
+  rg.publish(margin);
   if (mode == 0) {  // extract_lwe_locally (coefficient 0), detector.rs:561
     uint32_t *o = ext_out + g * (N1 + 1);
     for (int j = threadIdx.x; j < N1; j += 64 * W) o[j] = Lvl1Int::to_u32(j == 0 ? ext[0][0] : -ext[0][N1 - j]);
@@ -235,6 +239,21 @@ __global__ __launch_bounds__(64 * BR1L_WAVES, 1) void br1l_kernel(
       o[N1 + j] = Lvl1Int::to_u32(ext[1][j]);
     }
   }
+}
+
+__global__ __launch_bounds__(64 * BR1L_WAVES, 1) void br1l_kernel(
+    const uint16_t *__restrict__ clue_a, const uint16_t *__restrict__ clue_b,
+    const uint16_t *__restrict__ lwe_a, const uint16_t *__restrict__ lwe_b,
+    const double2 *__restrict__ bskl, DeviceTables tb, uint32_t *__restrict__ ext_out,
+    uint64_t *__restrict__ rlwe_out, int mode) {
+  br1l_body<false>(clue_a, clue_b, lwe_a, lwe_b, bskl, tb, ext_out, rlwe_out, mode, nullptr);
+}
+__global__ __launch_bounds__(64 * BR1L_WAVES, 1) void br1l_guard_kernel(
+    const uint16_t *__restrict__ clue_a, const uint16_t *__restrict__ clue_b,
+    const uint16_t *__restrict__ lwe_a, const uint16_t *__restrict__ lwe_b,
+    const double2 *__restrict__ bskl, DeviceTables tb, uint32_t *__restrict__ ext_out,
+    uint64_t *__restrict__ rlwe_out, int mode, unsigned long long *margin) {
+  br1l_body<true>(clue_a, clue_b, lwe_a, lwe_b, bskl, tb, ext_out, rlwe_out, mode, margin);
 }
 
 // ---- level 2 ---------------------------------------------------------------------------------

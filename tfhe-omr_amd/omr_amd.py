@@ -80,6 +80,10 @@ EXPORTS = {
     "omr_last_timing": (C.c_int, [C.c_void_p, C.POINTER(_Timing)]),
     "omr_detect_with_time_info": (C.c_int, [C.c_void_p, _u16p, _u16p, C.c_size_t, _u64p, C.POINTER(_Timing)]),
     "omr_ctx_check": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "omr_ctx_set_rounding_guard": (C.c_int, [C.c_void_p, C.c_int]),
+    "omr_ctx_rounding_margin": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]),
+    "omr_ctx_key_spectrum": (C.c_int, [C.c_void_p, C.c_int, C.c_size_t, C.c_size_t,
+                                       np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS")]),
     "omr_encode_indices": (C.c_int, [C.c_void_p, _u64p, C.c_size_t, C.c_size_t, C.c_size_t, C.c_uint64,
                                      C.c_uint32, _u64p]),
     "omr_encode_indices_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_size_t, C.c_size_t,
@@ -436,6 +440,23 @@ class Detector:
         """omr_ctx_check: sync `stream` (0: the whole device) and raise if an earlier call's device
         work failed."""
         _check(lib().omr_ctx_check(self._h, stream or None), "omr_ctx_check")
+
+    def set_rounding_guard(self, enable: bool = True):
+        """Run the guarded FFT kernel variants (same output) that record the rounding margin."""
+        _check(lib().omr_ctx_set_rounding_guard(self._h, int(bool(enable))), "omr_ctx_set_rounding_guard")
+
+    def rounding_margin(self, reset: bool = False) -> dict:
+        """{"observed": [level1, level2] largest |y - rint(y)| of the guarded runs so far,
+        "apriori": [E1, E2] proven bounds on |computed - exact|, "kappa": key-spectrum maxima}."""
+        obs, apr, kap = (C.c_double * 2)(), (C.c_double * 2)(), (C.c_double * 2)()
+        _check(lib().omr_ctx_rounding_margin(self._h, obs, apr, kap, int(bool(reset))), "omr_ctx_rounding_margin")
+        return {"observed": list(obs), "apriori": list(apr), "kappa": list(kap)}
+
+    def key_spectrum(self, level: int, first: int, count: int) -> np.ndarray:
+        """Stored key-spectrum values [count] complex (omr_ctx_key_spectrum)."""
+        out = np.zeros(2 * count, dtype=np.float64)
+        _check(lib().omr_ctx_key_spectrum(self._h, int(level), int(first), int(count), out), "omr_ctx_key_spectrum")
+        return out.view(np.complex128)
 
     def enable_timing(self, mode: int = 1):
         """0 off; 1 stage events around the production kernels (the throughput path fuses the

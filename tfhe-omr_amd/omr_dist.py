@@ -26,6 +26,58 @@ import numpy as np
 Q2 = 1125899906826241
 
 
+def launch_envs(gpus: int, environ, port: int, addr: str = "127.0.0.1"):
+    """Per-rank environments for a one-process-per-GPU run of `gpus` ranks, or None when this
+    process is already a rank (WORLD_SIZE set, e.g. by torch.distributed.run) or gpus == 1.
+    The reference sweeps worker counts inside one program (omr_time_analyze.rs:62-101); here
+    `bench.py --gpus N` without an external launcher starts N ranks itself. Raises ValueError
+    when WORLD_SIZE is set and disagrees with `gpus` (a SCALE record must not silently be a
+    1-GPU number)."""
+    if gpus < 1:
+        raise ValueError(f"--gpus must be >= 1, got {gpus}")
+    ws = environ.get("WORLD_SIZE")
+    if ws is not None and ws != "":
+        if int(ws) != gpus:
+            raise ValueError(f"--gpus {gpus} but WORLD_SIZE={ws}: the launcher and the flag disagree")
+        return None
+    if gpus == 1:
+        return None
+    envs = []
+    for r in range(gpus):
+        e = dict(environ)
+        e.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(gpus), LOCAL_WORLD_SIZE=str(gpus),
+                 MASTER_ADDR=addr, MASTER_PORT=str(port))
+        envs.append(e)
+    return envs
+
+
+def spawn_ranks(argv, envs, poll_s: float = 0.5) -> int:
+    """Start one child per environment running `argv` (stdout/stderr inherited: only rank 0
+    prints the result line) and wait for all of them. If any child fails, the others are
+    terminated and its exit code is returned; 0 when all succeed."""
+    import subprocess
+    procs = [subprocess.Popen(argv, env=e) for e in envs]
+    rc = 0
+    try:
+        while procs:
+            for p in list(procs):
+                code = p.poll()
+                if code is None:
+                    continue
+                procs.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code if code > 0 else 128 - code
+                    for q in procs:
+                        q.terminate()
+            time.sleep(poll_s)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+            p.wait()
+    return rc
+
+
 def shard_range(rank: int, world: int, total: int) -> tuple[int, int]:
     """Contiguous [first, first+count) of global message indices owned by `rank`."""
     base, rem = divmod(total, world)

@@ -1,5 +1,10 @@
 """Single-message (and small-batch) detect latency and its stage split (HIP events), on the
-bench's seeded keys. python tools/latency_split.py [D ...]"""
+bench's seeded keys. python tools/latency_split.py [D ...]
+With OMR_MAPS_OUT=<path> the process writes /proc/self/maps there just before it exits, so the
+PCs of an exit-time fault's stack (glog's "Aborted at" trace under rocprofv3) can be resolved to
+library + offset."""
+import atexit
+import os
 import sys
 import time
 
@@ -8,6 +13,12 @@ import numpy as np  # noqa: E402
 
 import product_lib as PL  # noqa: E402
 from product_lib import omr_amd as A  # noqa: E402
+
+if os.environ.get("OMR_MAPS_OUT"):
+    def _dump_maps(path=os.environ["OMR_MAPS_OUT"]):
+        with open("/proc/self/maps") as f, open(path, "w") as o:
+            o.write(f.read())
+    atexit.register(_dump_maps)  # registered first: runs last among the atexit hooks
 
 a, b, dk = PL.keys()
 det = A.Detector(dk)
