@@ -204,6 +204,19 @@ omr_status omr_ctx_set_encode_chunks(omr_ctx *ctx, size_t max_chunks);
  * out u64 [D][2][2048] (NTT domain). */
 omr_status omr_detect_batch(omr_ctx *ctx, const uint16_t *clue_a, const uint16_t *clue_b,
                             size_t D, uint64_t *out);
+/* Detector::detect (detector.rs:135-138) for one message: clue_a u16 [512], clue_b u16 [7],
+ * out u64 [2][2048]. Safe to call from many host threads at once on one context, as the
+ * reference's `clues.par_iter().map(|c| detector.detect(c))` does on a shared &Detector
+ * (examples/omr.rs:160-164): concurrent calls are coalesced into batched launches (whichever
+ * caller finds no launch in progress takes every queued request, up to max_messages, as one
+ * omr_detect_batch), so many callers reach batch throughput; a lone caller gets single-message
+ * latency. Each caller returns when its own output is written. */
+omr_status omr_detect(omr_ctx *ctx, const uint16_t *clue_a, const uint16_t *clue_b, uint64_t *out);
+/* Coalescing knobs of omr_detect: at most max_messages per combined launch (0 = 65,536), and a
+ * window (microseconds, default 0) a launching caller waits for more requests first. */
+omr_status omr_ctx_set_coalescing(omr_ctx *ctx, size_t max_messages, long window_us);
+/* omr_detect calls served and combined launches run so far on the context. */
+omr_status omr_ctx_coalescing_stats(omr_ctx *ctx, size_t *calls, size_t *launches);
 /* Same on device buffers, enqueued on `hip_stream` (NULL = HIP's null stream, which orders with
  * the other blocking streams, as in every HIP API); returns once enqueued. Calls on one context may use different streams: they share the
  * context's scratch, so a call's kernels wait (hipStreamWaitEvent) for those of the previous

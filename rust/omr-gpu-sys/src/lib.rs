@@ -19,7 +19,7 @@
 
 use std::ffi::CStr;
 use std::fmt;
-use std::os::raw::{c_char, c_int, c_void};
+use std::os::raw::{c_char, c_int, c_long, c_void};
 use std::time::Duration;
 
 /// Raw bindings of `include/omr_gpu.h`, one declaration per C entry point.
@@ -132,6 +132,9 @@ pub mod ffi {
         pub fn omr_ctx_set_encode_chunks(ctx: *mut OmrCtx, max_chunks: usize) -> OmrStatus;
         pub fn omr_detect_batch(ctx: *mut OmrCtx, clue_a: *const u16, clue_b: *const u16, d: usize,
                                 out: *mut u64) -> OmrStatus;
+        pub fn omr_detect(ctx: *mut OmrCtx, clue_a: *const u16, clue_b: *const u16, out: *mut u64) -> OmrStatus;
+        pub fn omr_ctx_set_coalescing(ctx: *mut OmrCtx, max_messages: usize, window_us: c_long) -> OmrStatus;
+        pub fn omr_ctx_coalescing_stats(ctx: *mut OmrCtx, calls: *mut usize, launches: *mut usize) -> OmrStatus;
         pub fn omr_detect_batch_device(ctx: *mut OmrCtx, d_clue_a: *const u16, d_clue_b: *const u16, d: usize,
                                        d_out: *mut u64, hip_stream: *mut c_void) -> OmrStatus;
         pub fn omr_ctx_enable_timing(ctx: *mut OmrCtx, mode: c_int) -> OmrStatus;
@@ -373,7 +376,11 @@ impl GpuDetector {
 
     /// `Detector::detect` (detector.rs:135-138): one clue set, a batch of one.
     pub fn detect(&self, clue: &Clue) -> Result<NttRlwe, OmrError> {
-        Ok(self.detect_batch(std::slice::from_ref(clue))?.pop().unwrap())
+        // omr_detect coalesces concurrent callers (e.g. rayon's par_iter over a shared &Detector,
+        // examples/omr.rs:160-164) into batched launches
+        let mut out = vec![0u64; 2 * OMR_N2];
+        check(unsafe { omr_detect(self.ctx, clue.a.as_ptr(), clue.b.as_ptr(), out.as_mut_ptr()) })?;
+        Ok(NttRlwe::from_flat(&out))
     }
 
     /// `clues.par_iter().map(|c| detector.detect(c))` (examples/omr.rs:160-164) in one call.
@@ -460,6 +467,12 @@ impl GpuDetector {
     /// At most `max_chunks` partial digests per encode ciphertext (0 = default 4,096).
     pub fn set_encode_chunks(&self, max_chunks: usize) -> Result<(), OmrError> {
         check(unsafe { omr_ctx_set_encode_chunks(self.ctx, max_chunks) })
+    }
+
+    /// Coalescing of concurrent `detect` callers (`omr_ctx_set_coalescing`): at most
+    /// `max_messages` per combined launch (0 = 65,536), launching after `window_us` microseconds.
+    pub fn set_coalescing(&self, max_messages: usize, window_us: i64) -> Result<(), OmrError> {
+        check(unsafe { omr_ctx_set_coalescing(self.ctx, max_messages, window_us as c_long) })
     }
 
     /// Rounding-margin guard of the FFT external products (`omr_ctx_set_rounding_guard`).

@@ -1,0 +1,55 @@
+"""Concurrent single-message detect() callers.
+
+The reference's driver calls `detector.detect(clue)` from every rayon thread on a shared
+&Detector (examples/omr.rs:160-164). omr_detect queues such calls on the context and runs every
+request queued while no launch is in progress as one batched detect, so an unchanged per-message
+caller reaches batch throughput: 64 host threads each call detect once; every output must equal
+the batched detect bit for bit, the calls must have been combined into few launches, and the
+aggregate rate must be at least 10x the one-at-a-time rate."""
+import threading
+import time
+
+import numpy as np
+import pytest
+
+import product_lib as PL
+from product_lib import omr_amd as A
+
+pytestmark = pytest.mark.gpu
+
+
+def test_concurrent_detect_calls_coalesce():
+    _, _, dk = PL.keys()
+    det = A.Detector(dk)
+    n = 64
+    mask = np.arange(n) % 9 == 0
+    ca, cb = PL.mixed_clues(mask, seed=4321)
+    want = det.detect_batch(ca, cb)
+    assert np.array_equal(det.detect(ca[0], cb[0]), want[0])  # warm, and one call alone
+    t = time.perf_counter()
+    for i in range(8):
+        det.detect(ca[i], cb[i])
+    seq = (time.perf_counter() - t) / 8
+    outs = [None] * n
+    go = threading.Barrier(n)
+
+    def call(i):
+        go.wait()
+        outs[i] = det.detect(ca[i], cb[i])
+
+    threads = [threading.Thread(target=call, args=(i,)) for i in range(n)]
+    calls0, launches0 = det.coalescing_stats()
+    t = time.perf_counter()
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join()
+    conc = time.perf_counter() - t
+    calls, launches = det.coalescing_stats()
+    det.close()
+    for i in range(n):
+        assert outs[i] is not None and np.array_equal(outs[i], want[i]), f"caller {i}"
+    print(f"\none at a time {seq * 1e3:.2f} ms/msg; {n} concurrent callers {conc * 1e3:.1f} ms total in "
+          f"{launches - launches0} launches: {seq * n / conc:.1f}x")
+    assert calls - calls0 == n and launches - launches0 <= n // 8
+    assert n / conc >= 10.0 / seq

@@ -8,6 +8,8 @@
 // launches per chunk: br1f_kernel (7 blind rotations per message), sum7_kernel, ks_mfma_kernel,
 // br2f_kernel (level-2 rotation on the exact FFT + the trace).
 #include <algorithm>
+#include <chrono>
+#include <condition_variable>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -285,6 +287,22 @@ struct omr_ctx {
   size_t timed_messages = 0, timed_chunks = 0;
   bool timed_split = false;  // the timed call ran the trace as its own launch in every chunk
   std::mutex mu;
+  // omr_detect: concurrent single-message calls are combined into batched launches (a leader
+  // takes every queued request, runs them as one detect, and wakes their callers)
+  struct DetectReq {
+    const uint16_t *a, *b;
+    uint64_t *out;
+    omr_status st;
+    std::string err;
+    bool done;
+  };
+  std::mutex qmu;
+  std::condition_variable qcv;
+  std::vector<DetectReq *> queue;
+  bool leader = false;
+  size_t coalesce_max = 65536;   // messages per combined launch
+  long coalesce_window_us = 0;   // a leader waits this long for more requests before launching
+  size_t coalesced_calls = 0, coalesced_launches = 0;
 };
 
 #define OMR_BR1_NAME "br1f_kernel"
@@ -984,6 +1002,76 @@ extern "C" omr_status omr_detect_batch(omr_ctx *c, const uint16_t *ca, const uin
   if (D == 0) return OMR_OK;
   std::lock_guard<std::mutex> lk(c->mu);
   return detect_host_locked(c, ca, cb, D, out);
+}
+
+// Detector::detect (detector.rs:135-138) for one message, callable from many host threads at once
+// (the reference's `clues.par_iter().map(|c| detector.detect(c))`, examples/omr.rs:160-164, on a
+// shared &Detector): the requests queue on the context; whichever caller finds no launch in
+// progress becomes the leader, optionally waits coalesce_window_us for more, gathers up to
+// coalesce_max queued clues into one omr_detect_batch (latency kernels up to the threshold,
+// throughput kernels above), scatters the outputs and wakes their callers; the next leader takes
+// what queued meanwhile. Every caller gets its batch's status and error message.
+extern "C" omr_status omr_detect(omr_ctx *c, const uint16_t *ca, const uint16_t *cb, uint64_t *out) {
+  if (!c || !ca || !cb || !out) return set_error(OMR_ERR_INVALID_ARGUMENT, "omr_detect: NULL argument");
+  omr_ctx::DetectReq r{ca, cb, out, OMR_OK, std::string(), false};
+  std::unique_lock<std::mutex> lk(c->qmu);
+  c->queue.push_back(&r);
+  c->qcv.notify_all();  // a leader inside its window may be waiting for a full batch
+  while (!r.done) {
+    if (c->leader) {
+      c->qcv.wait(lk);
+      continue;
+    }
+    c->leader = true;
+    if (c->coalesce_window_us > 0 && c->queue.size() < c->coalesce_max)
+      c->qcv.wait_for(lk, std::chrono::microseconds(c->coalesce_window_us),
+                      [&] { return c->queue.size() >= c->coalesce_max; });
+    const size_t n = std::min(c->queue.size(), c->coalesce_max);
+    std::vector<omr_ctx::DetectReq *> batch(c->queue.begin(), c->queue.begin() + (long)n);
+    c->queue.erase(c->queue.begin(), c->queue.begin() + (long)n);
+    lk.unlock();
+    std::vector<uint16_t> ga(n * N0), gb(n * CLUES);
+    std::vector<uint64_t> go(n * 2 * N2);
+    for (size_t k = 0; k < n; ++k) {
+      memcpy(&ga[k * N0], batch[k]->a, N0 * sizeof(uint16_t));
+      memcpy(&gb[k * CLUES], batch[k]->b, CLUES * sizeof(uint16_t));
+    }
+    omr_status st;
+    {
+      std::lock_guard<std::mutex> dl(c->mu);
+      st = detect_host_locked(c, ga.data(), gb.data(), n, go.data());
+    }
+    const std::string err = st == OMR_OK ? std::string() : std::string(omr_last_error());
+    for (size_t k = 0; k < n; ++k)
+      if (st == OMR_OK) memcpy(batch[k]->out, &go[k * 2 * N2], 2 * N2 * sizeof(uint64_t));
+    lk.lock();
+    for (auto *q : batch) {
+      q->st = st;
+      q->err = err;
+      q->done = true;
+    }
+    c->coalesced_calls += n;
+    c->coalesced_launches += 1;
+    c->leader = false;
+    c->qcv.notify_all();
+  }
+  return r.st == OMR_OK ? OMR_OK : set_error(r.st, r.err);
+}
+
+extern "C" omr_status omr_ctx_set_coalescing(omr_ctx *c, size_t max_messages, long window_us) {
+  if (!c || window_us < 0) return set_error(OMR_ERR_INVALID_ARGUMENT, "omr_ctx_set_coalescing: bad argument");
+  std::lock_guard<std::mutex> lk(c->qmu);
+  c->coalesce_max = max_messages ? max_messages : 65536;
+  c->coalesce_window_us = window_us;
+  return OMR_OK;
+}
+
+extern "C" omr_status omr_ctx_coalescing_stats(omr_ctx *c, size_t *calls, size_t *launches) {
+  if (!c) return set_error(OMR_ERR_INVALID_ARGUMENT, "omr_ctx_coalescing_stats: NULL ctx");
+  std::lock_guard<std::mutex> lk(c->qmu);
+  if (calls) *calls = c->coalesced_calls;
+  if (launches) *launches = c->coalesced_launches;
+  return OMR_OK;
 }
 
 namespace {

@@ -75,6 +75,9 @@ EXPORTS = {
     "omr_ctx_set_latency_threshold": (C.c_int, [C.c_void_p, C.c_size_t]),
     "omr_ctx_set_encode_chunks": (C.c_int, [C.c_void_p, C.c_size_t]),
     "omr_detect_batch": (C.c_int, [C.c_void_p, _u16p, _u16p, C.c_size_t, _u64p]),
+    "omr_detect": (C.c_int, [C.c_void_p, _u16p, _u16p, _u64p]),
+    "omr_ctx_set_coalescing": (C.c_int, [C.c_void_p, C.c_size_t, C.c_long]),
+    "omr_ctx_coalescing_stats": (C.c_int, [C.c_void_p, C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)]),
     "omr_detect_batch_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p]),
     "omr_ctx_enable_timing": (C.c_int, [C.c_void_p, C.c_int]),
     "omr_last_timing": (C.c_int, [C.c_void_p, C.POINTER(_Timing)]),
@@ -419,7 +422,21 @@ class Detector:
 
     # detect (detector.rs:135) — one clue set -> NttRlweCiphertext [2][2048]
     def detect(self, clue_a, clue_b) -> np.ndarray:
-        return self.detect_batch(np.asarray(clue_a).reshape(1, N0), np.asarray(clue_b).reshape(1, CLUE_COUNT))[0]
+        """One message (omr_detect): thread-safe; concurrent callers are coalesced into batched
+        launches (ctypes releases the GIL during the call)."""
+        a = np.ascontiguousarray(clue_a, dtype=np.uint16).reshape(N0)
+        b = np.ascontiguousarray(clue_b, dtype=np.uint16).reshape(CLUE_COUNT)
+        out = np.empty((2, N2), np.uint64)
+        _check(lib().omr_detect(self._h, a, b, out.reshape(-1)), "omr_detect")
+        return out
+
+    def set_coalescing(self, max_messages: int = 0, window_us: int = 0):
+        _check(lib().omr_ctx_set_coalescing(self._h, int(max_messages), int(window_us)), "omr_ctx_set_coalescing")
+
+    def coalescing_stats(self) -> tuple:
+        calls, launches = C.c_size_t(), C.c_size_t()
+        _check(lib().omr_ctx_coalescing_stats(self._h, C.byref(calls), C.byref(launches)), "omr_ctx_coalescing_stats")
+        return calls.value, launches.value
 
     def detect_batch(self, clue_a, clue_b) -> np.ndarray:
         clue_a = np.ascontiguousarray(clue_a, dtype=np.uint16)
