@@ -222,6 +222,9 @@ double apriori_bound(int level, double kappa) {
 
 }  // namespace
 
+#ifndef OMR_BR2Y
+#define OMR_BR2Y 0
+#endif
 #ifndef OMR_DEFAULT_LATENCY_MAX
 #define OMR_DEFAULT_LATENCY_MAX 64  // chunks up to this many messages run the latency kernels
 #endif
@@ -532,8 +535,12 @@ omr_status launch_br2x(omr_ctx *c, size_t n, const uint32_t *lwe_int, uint64_t *
   int *err = c->x_err;
   void *args[] = {(void *)&lwe_int, (void *)&bsk2, (void *)&tb, (void *)&slots, (void *)&flags, (void *)&err,
                   (void *)&out};
-  const hipError_t e = hipLaunchCooperativeKernel(reinterpret_cast<const void *>(&br2x_kernel),
-                                                  dim3((unsigned)(2 * n)), dim3(BR2L_T), args, 0, st);
+#if OMR_BR2Y  // both groups of each CU share the partial combination, hand-off and inverse
+  const void *kern = reinterpret_cast<const void *>(&br2y_kernel);
+#else
+  const void *kern = reinterpret_cast<const void *>(&br2x_kernel);
+#endif
+  const hipError_t e = hipLaunchCooperativeKernel(kern, dim3((unsigned)(2 * n)), dim3(BR2L_T), args, 0, st);
   if (e == hipErrorCooperativeLaunchTooLarge || e == hipErrorNotSupported || e == hipErrorInvalidConfiguration) {
     (void)hipGetLastError();  // refused: nothing was enqueued
     return OMR_OK;

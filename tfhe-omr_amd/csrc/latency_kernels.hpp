@@ -545,6 +545,245 @@ __global__ __launch_bounds__(BR2L_T, 1) void br2x_kernel(const uint32_t *__restr
   }
 }
 
+// ---- level 2 over two CUs, the inverse split over both groups (br2y_kernel) -----------------
+// br2x_kernel leaves group 1 idle while group 0 combines the partials, hands off the partner's
+// output and runs the inverse (the last ~25 % of a step). Here both groups do half of that: after
+// its multiply-accumulate each group applies inverse stage 10 (index bit 0, register bit 1 of e in
+// CmuxNtt's P3 layout) to its own partials (linear, so the sums commute with it), and then owns the
+// positions with index bit 0 == g, which stages 9..0 never combine with the other half: it takes
+// the other group's partials for them through LDS, hands off / receives that half of the partner
+// CU's output, and runs stages 9..0 of its 1024-point half on 256 threads x 4 registers
+// (HalfInv). ACC_r is then held split: thread t of group g keeps coefficients 2 t + g + 512 f.
+// tests/test_half_inverse_layout.py restates the layouts and checks the split inverse against the
+// full one with exact integers.
+struct HalfInv {
+  using M = Mod<2>;
+  static constexpr int T = 256, F = 4;
+  // index bit 10 - s of inverse stage s sits on register bit h(s) of every layout below
+  OMR_HD static constexpr int h_of(int s) { return s == 9 ? 2 : s == 8 ? 1 : (s & 1) ? 1 : 2; }
+  // index held by register f of thread t of group g in layout Q<p> (tests/test_half_inverse_layout.py jq)
+  OMR_HD static constexpr int jq(int p, int g, int t, int f) {
+    const int f0 = f & 1, f1 = (f >> 1) & 1;
+    const int t0 = t & 1, t1 = (t >> 1) & 1, t2 = (t >> 2) & 1, t3 = (t >> 3) & 1, t4 = (t >> 4) & 1,
+              t5 = (t >> 5) & 1, t6 = (t >> 6) & 1, t7 = (t >> 7) & 1;
+    const int hi = (t6 << 9) | (t7 << 10);
+    return g | (p == 0 ? (f1 << 1) | (f0 << 2) | (t4 << 3) | (t5 << 4) | ((t & 15) << 5) | hi
+              : p == 1 ? (t5 << 1) | (t4 << 2) | (f0 << 3) | (f1 << 4) | ((t & 15) << 5) | hi
+              : p == 2 ? (t3 << 1) | (t2 << 2) | (t1 << 3) | (t0 << 4) | (f0 << 5) | (f1 << 6) | (t4 << 7) | (t5 << 8) | hi
+              : p == 3 ? (t3 << 1) | (t2 << 2) | (t1 << 3) | (t0 << 4) | (t4 << 5) | (t5 << 6) | (f0 << 7) | (f1 << 8) | hi
+                       : (t << 1) | (f << 9));
+  }
+  // P3 register of half register f of group g (layout Q0 is P3 restricted to e bit 1 == g)
+  OMR_HD static constexpr int e_of(int g, int f) { return (f & 1) | (g << 1) | ((f >> 1) << 2); }
+  // inverse stage S on layout P; tw: the CmuxNtt table in LDS (tw2c: stage 9 read through its
+  // permuted slot, stages <= 8 are the plain mirrored tree)
+  template <int P, int S>
+  __device__ static __forceinline__ void stage(double (&x)[F], const double *tw, int g, int t, int &since_red) {
+    constexpr int h = h_of(S);
+    if (since_red >= M::RED_INV) {
+#pragma unroll
+      for (int f = 0; f < F; ++f) x[f] = red<M>(x[f]);
+      since_red = 0;
+    }
+#pragma unroll
+    for (int f = 0; f < F; ++f) {
+      if (f & h) continue;
+      const int slot = S == 9 ? (2 << 9) - 1 - ((f & 1) * 256 + t) : (2 << S) - 1 - (jq(P, g, t, f) >> (11 - S));
+      const double w = tw[slot];
+      const double u = x[f], v = x[f + h];
+      x[f] = u + v;
+      x[f + h] = mm<M>(v - u, w);
+    }
+    ++since_red;
+  }
+  __device__ static __forceinline__ void perm(double (&x)[F]) {  // register bit 0 <-> lane bit 4, bit 1 <-> lane bit 5
+    swap_lane_bit<4>(x[0], x[1]);
+    swap_lane_bit<4>(x[2], x[3]);
+    swap_lane_bit<5>(x[0], x[2]);
+    swap_lane_bit<5>(x[1], x[3]);
+  }
+  // wave-local Q1 -> Q2 slot of index j within the wave's 256 (k = j >> 1 bits 0..7): conflict
+  // free for the ds_write_b64 16-lane groups of Q1 (k4..k7 vary) and the ds_read_b64 32-lane
+  // groups of Q2 (k0..k3, k6 vary)
+  OMR_HD static constexpr int wslot(int j) {
+    const int k = (j >> 1) & 255;
+    const int b[8] = {(k & 1) ^ ((k >> 4) & 1), ((k >> 1) & 1) ^ ((k >> 5) & 1), ((k >> 2) & 1) ^ ((k >> 6) & 1),
+                      ((k >> 3) & 1) ^ ((k >> 7) & 1), (k >> 6) & 1, (k >> 4) & 1, (k >> 5) & 1, (k >> 7) & 1};
+    int s = 0;
+    for (int i = 0; i < 8; ++i) s |= b[i] << i;
+    return ((j >> 9) << 8) | s;
+  }
+  // stages 9..0 of group g's half: in Q0 (P3 registers e_of(g, f)), out Q4 (coefficient 2 t + g + 512 f).
+  // W: the group's wave-local buffer (1024 doubles), X: its cross-wave buffer (1024 doubles; one
+  // workgroup barrier, both groups reach it together)
+  __device__ static __forceinline__ void inv(double (&x)[F], double *X, double *W, const double *tw, int g, int t) {
+    int sr = 0;
+    stage<0, 9>(x, tw, g, t, sr);
+    stage<0, 8>(x, tw, g, t, sr);
+    perm(x);
+    stage<1, 7>(x, tw, g, t, sr);
+    stage<1, 6>(x, tw, g, t, sr);
+#pragma unroll
+    for (int f = 0; f < F; ++f) W[wslot(jq(1, g, t, f))] = x[f];
+    WgNtt<M, 256, 8>::wave_sync();
+#pragma unroll
+    for (int f = 0; f < F; ++f) x[f] = W[wslot(jq(2, g, t, f))];
+    __builtin_amdgcn_wave_barrier();
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    stage<2, 5>(x, tw, g, t, sr);
+    stage<2, 4>(x, tw, g, t, sr);
+    perm(x);
+    stage<3, 3>(x, tw, g, t, sr);
+    stage<3, 2>(x, tw, g, t, sr);
+#pragma unroll
+    for (int f = 0; f < F; ++f) X[jq(3, g, t, f) >> 1] = x[f];
+    wg_barrier_lds();
+#pragma unroll
+    for (int f = 0; f < F; ++f) x[f] = X[jq(4, g, t, f) >> 1];
+    __builtin_amdgcn_wave_barrier();
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    stage<4, 1>(x, tw, g, t, sr);
+    stage<4, 0>(x, tw, g, t, sr);
+  }
+};
+
+__global__ __launch_bounds__(BR2L_T, 1) void br2y_kernel(const uint32_t *__restrict__ lwe_int,
+                                                         const double *__restrict__ bsk2, DeviceTables tb,
+                                                         double *xg, uint32_t *flags, int *err,
+                                                         uint64_t *__restrict__ out) {
+  using M = Mod<2>;
+  constexpr int T = BR2_T, E = BR2_E, N = N2, F = HalfInv::F;
+  using NTT = CmuxNtt;
+  using DG = Digits2;
+  constexpr int KD = D2 / 2;  // digits per group
+  __shared__ double xbuf[2][NTT::LDS_DOUBLES];
+  __shared__ double part[2][N];  // [output][other half of each group: (1 - g) * 1024 + f * 256 + t]
+  __shared__ double tws[N + 136 * 5];
+  __shared__ int stop;
+  const int m = blockIdx.x >> 1, r = blockIdx.x & 1;
+  const int g = threadIdx.x / T, t = threadIdx.x % T;
+  double *X = xbuf[g];
+  double *ST = xbuf[0] + N;  // the staged accumulator (group 0's X1), written by both groups
+  const double *tw = tws, *t0 = tws + N;
+  const uint32_t *lwe = lwe_int + (size_t)m * (NI + 1);
+  double acc[F];  // ACC_r coefficients 2 t + g + 512 f
+  {
+    const int b = (int)lwe[NI];
+    const int rr = (2 * N - (b % (2 * N))) % (2 * N);
+#pragma unroll
+    for (int f = 0; f < F; ++f) acc[f] = r == 1 ? canon_small<M>(rot_read<N>(tb.lut2, HalfInv::jq(4, g, t, f), rr)) : 0.0;
+    for (int j = threadIdx.x; j < N; j += BR2L_T) tws[j] = tb.tw2c[j];
+    if (threadIdx.x <= 128) {  // table k: d * c_k, d = tid - 64 (c = tw1, tw2, tw1 tw2, tw3, tw1 tw3)
+      const double w1 = tb.tw2[1], w2 = tb.tw2[2], w3 = tb.tw2[3];
+      const double c[5] = {w1, w2, canon<M>(mm<M>(w1, w2)), w3, canon<M>(mm<M>(w1, w3))};
+#pragma unroll
+      for (int k = 0; k < 5; ++k)
+        tws[N + 136 * k + threadIdx.x] = canon<M>(mm<M>((double)((int)threadIdx.x - 64), c[k]));
+    }
+    if (threadIdx.x == 0) stop = 0;
+    __syncthreads();
+  }
+  uint32_t *my_flag = flags + 2 * m + r, *their_flag = flags + 2 * m + (1 - r);
+  uint32_t hc = 0;  // hand-offs so far (executed steps)
+#pragma unroll 1
+  for (int i = 0; i < NI; ++i) {
+    const int a = (int)__builtin_amdgcn_readfirstlane(lwe[i]) & (2 * N - 1);
+    if (a == 0) continue;  // (X^0 - 1) * ACC = 0 (both workgroups of the message skip it)
+    const size_t slot = hc & 1;
+    const double *ggsw = bsk2 + ((size_t)i * 2 * D2 + (size_t)r * D2 + (size_t)g * KD) * 2 * N;
+    uint32_t pk[E][DG::DW];
+    {  // digits of (X^a - 1) * ACC_r: both groups stage their halves, both decompose all of it
+#pragma unroll
+      for (int f = 0; f < F; ++f) ST[HalfInv::jq(4, g, t, f)] = acc[f];
+      __syncthreads();
+#pragma unroll
+      for (int e = 0; e < E; ++e)
+        DG::pack(canon_small<M>(rot_read_lds<N>(ST, t + e * T, a) - ST[t + e * T]), pk[e]);
+      __builtin_amdgcn_wave_barrier();
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    }
+    double accA[E], accB[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) accA[e] = accB[e] = 0.0;
+    KeyRow<double, E> cur;
+    cur.load(ggsw, N, t * E);
+#pragma unroll
+    for (int h = 0; h < KD; ++h) {  // three digits: X0, X1, X0 (the staging used group 0's X1)
+      const int k = g * KD + h;
+      double x[E];
+      int fd[E];
+#pragma unroll
+      for (int e = 0; e < E; ++e) fd[e] = DG::get_int(pk[e], k) + 64;
+      if ((h & 1) == 0)
+        NTT::template fwd_small<0>(fd, t0, x, X, tw, t, tb.tw2c);
+      else
+        NTT::template fwd_small<1>(fd, t0, x, X, tw, t, tb.tw2c);
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        accA[e] += mm<M>(x[e], cur.a[e]);
+        accB[e] += mm<M>(x[e], cur.b[e]);
+      }
+      if (h + 1 < KD) cur.load(ggsw + (size_t)(h + 1) * 2 * N, N, t * E);
+    }
+    // inverse stage 10 on this group's partials (three products on a zero sum: |.| < 5.3q)
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      accA[e] = red<M>(accA[e]);
+      accB[e] = red<M>(accB[e]);
+    }
+    {
+      int sr = 0;
+      NTT::template stage<3, 10, true>(accA, tw, t, sr);
+      sr = 0;
+      NTT::template stage<3, 10, true>(accB, tw, t, sr);
+    }
+    // the other group's half of both outputs through LDS (lane-contiguous)
+#pragma unroll
+    for (int f = 0; f < F; ++f) {
+      const int e = HalfInv::e_of(1 - g, f);
+      part[0][(1 - g) * 1024 + f * T + t] = red<M>(accA[e]);
+      part[1][(1 - g) * 1024 + f * T + t] = red<M>(accB[e]);
+    }
+    __syncthreads();
+    double keep[F];
+#pragma unroll
+    for (int f = 0; f < F; ++f) {
+      const int e = HalfInv::e_of(g, f);
+      const double sa = red<M>(red<M>(accA[e]) + part[0][g * 1024 + f * T + t]);
+      const double sb = red<M>(red<M>(accB[e]) + part[1][g * 1024 + f * T + t]);
+      keep[f] = r == 0 ? sa : sb;
+      st_sc1(xg + (((size_t)m * 2 + r) * 2 + slot) * N + g * 1024 + f * T + t, r == 0 ? sb : sa);  // the partner's output
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __hip_atomic_store(my_flag, hc + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      int n = 0;
+      while (__hip_atomic_load(their_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < hc + 1) {
+        if (++n == BR2X_SPIN) {
+          stop = 1;
+          atomicExch(err, 1);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+    }
+    __syncthreads();
+    if (stop) break;
+    double s[F];
+#pragma unroll
+    for (int f = 0; f < F; ++f)
+      s[f] = red<M>(keep[f] + ld_sc1(xg + (((size_t)m * 2 + (1 - r)) * 2 + slot) * N + g * 1024 + f * T + t));
+    HalfInv::inv(s, X, X + 2 * N, tw, g, t);
+#pragma unroll
+    for (int f = 0; f < F; ++f) acc[f] = canon<M>(acc[f] + s[f]);
+    ++hc;
+  }
+  uint64_t *o = out + (size_t)m * 2 * N + (size_t)r * N;
+#pragma unroll
+  for (int f = 0; f < F; ++f) o[HalfInv::jq(4, g, t, f)] = to_u64<M>(acc[f]);
+}
+
 // hom_trace (detector.rs:626-639) in place on blind-rotation outputs (coefficient domain,
 // canonical u64 [2][N2] per message) -> NttRlweCiphertext u64 [2][N2].
 __global__ __launch_bounds__(BR2_T, 2) void trace_kernel(uint64_t *__restrict__ io, const double *__restrict__ tk,
