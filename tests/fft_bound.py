@@ -1,0 +1,46 @@
+"""A priori bound on the rounding error of the FFT external products, restated
+from the coefficient-domain key with numpy -- the same formula context.hip's apriori_bound
+evaluates on the device-stored double-double key spectra at context creation:
+
+  E = n D (1 + 2^-30) max over steps i and output spectra o of
+      [(2 delta_f + u (1 + 2^-40)) sum_r kappa_{i,r,o} + sqrt(2) u sum_k (2R - 2k) kappa_{i,r(k),o}]
+
+n complex points, R GGSW rows accumulated in the order r(0), r(1), ..., D = sqrt(2n) d_max,
+delta_f = 26u, kappa_{i,r,o} = max_j |K_{i,r,o}[j]| (spectrum of key row r of step i, output o;
+level 2: per 25-bit limb). Spectral magnitudes do not depend on the output order, so a plain
+twisted DFT gives them: K[m] = (1/n) sum_k z_k e^{i pi k / 2n} e^{2 pi i k m / n}."""
+import numpy as np
+
+U = 2.0 ** -53
+ORDER2 = [0, 3, 1, 4, 2, 5, 6, 9, 7, 10, 8, 11]  # br2f_kernel's digit issue order
+
+
+def _centred(v, q):
+    v = v.astype(np.int64)
+    return np.where(v > (q - 1) // 2, v - q, v).astype(np.float64)
+
+
+def _row_max(rows, n):
+    tw = np.exp(1j * np.pi * np.arange(n) / (2 * n))
+    z = rows[..., :n] + 1j * rows[..., n:]
+    return np.abs(np.fft.fft(z * tw, axis=-1)).max(axis=-1) / n
+
+
+def _bound(kmax, n, R, dmax, order):
+    """kmax [steps][R][outputs]"""
+    k = kmax[:, order, :]
+    w = (2.0 * R - 2.0 * np.arange(R))[None, :, None]
+    inner = (2 * 26 * U + U * (1 + 2.0 ** -40)) * k.sum(axis=1) + np.sqrt(2.0) * U * (w * k).sum(axis=1)
+    return n * np.sqrt(2.0 * n) * dmax * inner.max() * (1 + 2.0 ** -30)
+
+
+def apriori_bounds(dk, q1=134215681, q2=1125899906826241):
+    """(E1, E2, kappa1, kappa2) for a DetectionKey (omr_amd.DetectionKey layout)."""
+    r1 = _centred(dk.bsk1.reshape(512, 8, 2, 1024), q1)
+    k1 = _row_max(r1, 512)                                   # [512][8][2]
+    r2 = _centred(dk.bsk2.reshape(670, 12, 2, 2048), q2)
+    hi = np.rint(r2 / 2.0 ** 25)
+    k2 = np.stack([_row_max(r2 - hi * 2.0 ** 25, 1024), _row_max(hi, 1024)], axis=-1).reshape(670, 12, 4)
+    e1 = _bound(k1, 512, 8, 16.0, list(range(8)))
+    e2 = _bound(k2, 1024, 12, 64.0, ORDER2)
+    return e1, e2, float(k1.max()), float(k2.max())

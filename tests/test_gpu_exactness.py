@@ -8,7 +8,8 @@ rounding exact on bench.py's own keys and clues (pack 42, key seed 7, clue seeds
 - the rounding-margin guard (exactness.hpp) over one 65,536-message launch: the largest
   |y - rint(y)| of every rounded coefficient of both levels is < 0.1, the guarded output equals
   the production output, and the run is certified by the a priori bound (observed < 1 - E);
-- the level-1 a priori bound alone is < 0.5 (exact for every input on this key);
+- the a priori bounds the library computes from its stored key spectra equal the numpy
+  restatement (tests/fft_bound.py) and are < 0.5 on both levels: exact for every input on this key;
 - the same 65,536 clues through the latency family with the threshold raised, so level 2 runs
   br2l_kernel's exact modular NTT (and trace_kernel): all 65,536 outputs bit-identical to the
   throughput family's;
@@ -77,7 +78,12 @@ def test_rounding_margin_full_launch_certified(full):
     print(f"\nrounding margin over {D_FULL} messages: level 1 {obs[0]:.3e}, level 2 {obs[1]:.3e}; "
           f"a priori bounds {apr[0]:.3f}, {apr[1]:.3f}; kappa {m['kappa']}")
     assert 0 < obs[0] < 0.1 and 0 < obs[1] < 0.1
-    assert apr[0] < 0.5, "level 1: exact for every input on this key"
+    # the library's bound on its stored (double-double) spectra equals the numpy restatement
+    from fft_bound import apriori_bounds
+    e1, e2, k1, k2 = apriori_bounds(PL.keys()[2])
+    assert abs(apr[0] - e1) < 1e-9 * e1 and abs(apr[1] - e2) < 1e-9 * e2, (apr, e1, e2)
+    assert abs(m["kappa"][0] - k1) < 1e-9 * k1 and abs(m["kappa"][1] - k2) < 1e-9 * k2
+    assert apr[0] < 0.5 and apr[1] < 0.5, "both levels exact for every input on this key"
     for lvl in range(2):
         assert obs[lvl] < 1 - apr[lvl], f"level {lvl + 1}: run not certified"
 

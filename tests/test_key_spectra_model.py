@@ -67,3 +67,15 @@ def test_tree_inverse_gives_negacyclic_product():
     got = np.rint(M2.unfold(prod)).astype(np.int64)
     want = np.array(M2.negacyclic(a, k), dtype=np.int64)
     assert np.array_equal(got, want)
+
+
+def test_apriori_bound_proves_both_levels_exact_on_the_bench_key():
+    """On bench.py's key (pack 42, key seed 7) the a priori bound is below 0.5 for both levels, so
+    rounding every FFT product coefficient recovers the exact integer for every input
+    (the library evaluates the same bound on its stored spectra, checked against
+    this restatement in tests/test_gpu_exactness.py)."""
+    import product_lib as PL
+    from fft_bound import apriori_bounds
+    e1, e2, k1, k2 = apriori_bounds(PL.keys()[2])
+    assert e1 < 0.15 and e2 < 0.45, (e1, e2)
+    assert 5e6 < k1 < 2e7 and 1e6 < k2 < 3e6  # ~4 sigma of uniform keys' spectra

@@ -206,18 +206,37 @@ std::vector<CDD> dd_tree_twiddles(int L) {
 }
 
 // A priori bound on |computed - exact| of every rounded coefficient of one external product
-// (DESIGN.md §3): E = n R D kappa (2 delta_f + sqrt(2) (R + 1) u + u (1 + 2^-40)), with n complex
-// points, R GGSW rows, D = sqrt(2n) d_max the 2-norm bound of a digit polynomial, delta_f = 26u the
-// forward / inverse transform's relative 2-norm error (5u per radix-4 pass, 8u per radix-8, 4u
-// per radix-2, rounded up), the sequential fma accumulation over R rows, and the double-double
-// keys' |K^ - K| <= u |K|.
-double apriori_bound(int level, double kappa) {
+// (DESIGN.md §3a). For one CMUX step and one output spectrum, with n complex points, D =
+// sqrt(2n) d_max the 2-norm bound of a digit polynomial, kappa_r the largest |K^| of GGSW row r
+// (row_max_abs_kernel), the rows accumulated in the order r(0), r(1), ... by two fmas each:
+//   E = n D (1 + 2^-30) [(2 delta_f + u (1 + 2^-40)) sum_r kappa_r + sqrt(2) u sum_k (2R - 2k) kappa_r(k)]
+// forward digit transforms and the inverse each within delta_f = 26u relative 2-norm error (5u per
+// radix-4 pass, 8u per radix-8, 4u per radix-2, rounded up), the sequential fma accumulation, and
+// the double-double keys' |K^ - K| <= u |K|. The maximum over every step and output spectrum.
+// kmax: [steps][rows][outputs] (level 1: [512][8][2]; level 2: [670][12][2 out][2 limb], the limbs
+// as two more "outputs").
+double apriori_bound(int level, const std::vector<double> &kmax) {
   const double u = 0x1p-53;
-  const int n = level == 1 ? 512 : 1024, R = level == 1 ? 2 * D1 : 2 * D2;
-  const double dmax = level == 1 ? 16.0 : 64.0;
-  const double D = std::sqrt(2.0 * n) * dmax;
-  const double coef = 2 * 26 * u + std::sqrt(2.0) * (R + 1) * u + u * (1 + 0x1p-40);
-  return (double)n * R * D * kappa * (1 + 0x1p-40) * coef;
+  const int n = level == 1 ? 512 : 1024, R = level == 1 ? 2 * D1 : 2 * D2, O = level == 1 ? 2 : 4;
+  const int steps = level == 1 ? N0 : NI;
+  // accumulation order of the kernels' MAC: br1f / br1l rows 0..7; br2f digits in issue order
+  // g = 2 j + w, row p D2 + j + 3 w (br2_fft.hpp)
+  const int order2[12] = {0, 3, 1, 4, 2, 5, 6, 9, 7, 10, 8, 11};
+  const double D = std::sqrt(2.0 * n) * (level == 1 ? 16.0 : 64.0);
+  const double cf = 2 * 26 * u + u * (1 + 0x1p-40), cw = std::sqrt(2.0) * u;
+  double worst = 0.0;
+  for (int i = 0; i < steps; ++i)
+    for (int o = 0; o < O; ++o) {
+      double s = 0.0, w = 0.0;
+      for (int k = 0; k < R; ++k) {
+        const int r = level == 1 ? k : order2[k];
+        const double kap = kmax[((size_t)i * R + r) * O + o];
+        s += kap;
+        w += (2.0 * R - 2.0 * k) * kap;
+      }
+      worst = std::max(worst, cf * s + cw * w);
+    }
+  return (double)n * D * worst * (1 + 0x1p-30);
 }
 
 }  // namespace
@@ -735,22 +754,26 @@ extern "C" omr_status omr_ctx_create(const omr_detection_key_view *key, int devi
   if ((st = convert_keys_cmux(key->bsk2, BSK2_ELEMS / N2, c->bsk2, ninv2, c->tb.tw2c, c->stream)) != OMR_OK)
     return fail(st);
   if ((st = convert_keys_dd<2>(key->bsk2, BSK2_ELEMS / N2, c->bsk2f, c->stream)) != OMR_OK) return fail(st);
-  {  // kappa per level (the a priori bound's key constant) and the guard's margin words
-    if (hipMalloc(&c->margin, 4 * sizeof(unsigned long long)) != hipSuccess)
+  {  // kappa_r per key row (the a priori bound's key constants) and the guard's margin words
+    const size_t rows1 = BSK1_ELEMS / 2 / Fft512::N, rows2 = BSK2_ELEMS / Fft1024::n;
+    DevBufHost<double> km;
+    if (hipMalloc(&c->margin, 2 * sizeof(unsigned long long)) != hipSuccess ||
+        hipMalloc(&km.p, (rows1 + rows2) * sizeof(double)) != hipSuccess)
       return fail(set_error(OMR_ERR_OUT_OF_MEMORY, "omr_ctx_create: margin words"));
-    const bool ok = hipMemsetAsync(c->margin, 0, 4 * sizeof(unsigned long long), c->stream) == hipSuccess;
+    const bool ok = hipMemsetAsync(c->margin, 0, 2 * sizeof(unsigned long long), c->stream) == hipSuccess;
     if (ok) {
-      max_abs_kernel<<<1024, 256, 0, c->stream>>>(c->bsk1f, BSK1_ELEMS / 2, c->margin + 2);
-      max_abs_kernel<<<2048, 256, 0, c->stream>>>(c->bsk2f, BSK2_ELEMS, c->margin + 3);
+      row_max_abs_kernel<<<(unsigned)rows1, 256, 0, c->stream>>>(c->bsk1f, Fft512::N, km.p);
+      row_max_abs_kernel<<<(unsigned)rows2, 256, 0, c->stream>>>(c->bsk2f, Fft1024::n, km.p + rows1);
     }
-    unsigned long long w[2] = {0, 0};
+    std::vector<double> k1(rows1), k2(rows2);
     if (!ok || hipGetLastError() != hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess ||
-        hipMemcpy(w, c->margin + 2, sizeof(w), hipMemcpyDeviceToHost) != hipSuccess)
+        hipMemcpy(k1.data(), km.p, rows1 * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(k2.data(), km.p + rows1, rows2 * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess)
       return fail(set_error(OMR_ERR_DEVICE, "omr_ctx_create: key spectrum maxima"));
-    for (int l = 0; l < 2; ++l) {
-      c->kappa[l] = __builtin_bit_cast(double, w[l]);
-      c->apriori[l] = apriori_bound(l + 1, c->kappa[l]);
-    }
+    c->kappa[0] = *std::max_element(k1.begin(), k1.end());
+    c->kappa[1] = *std::max_element(k2.begin(), k2.end());
+    c->apriori[0] = apriori_bound(1, k1);
+    c->apriori[1] = apriori_bound(2, k2);
   }
   if ((st = convert_keys<2, uint64_t, double>(key->trace_key, TK_ELEMS / N2, c->tk, 1.0, c->tb.tw2,
                                               c->stream)) != OMR_OK)

@@ -8,9 +8,10 @@
 //    radix-2 tree FFT in double-double arithmetic with double-double twiddles (accuracy ~2^-100)
 //    and rounded once to FP64, so every stored spectral value K^ obeys |K^ - K| <= u |K| (u = 2^-53)
 //    instead of carrying an FP64 transform error (key_spectrum_dd_kernel);
-//  - kappa, the largest |K^| of each level's stored keys (max_abs_kernel): the only key-dependent
-//    constant of the a priori bound E = n R D kappa (2 delta_f + sqrt(2) (R + 1) u + u (1 + 2^-40))
-//    on |computed - exact| of every rounded product coefficient (context.hip: apriori_bound);
+//  - kappa_r, the largest |K^| of every stored key row (row_max_abs_kernel): the only key-dependent
+//    constants of the a priori bound on |computed - exact| of every rounded product coefficient,
+//    E = n D max over steps and outputs of [(2 delta_f + u') sum_r kappa_r + sqrt(2) u sum_k w_k
+//    kappa_r(k)] (context.hip: apriori_bound);
 //  - the rounding-margin guard (RoundGuard): the guarded kernel variants record the largest
 //    |y - rint(y)| over every rounded product coefficient and publish it with one 64-bit atomic
 //    max per wave. If E < 0.5 the rounding is exact for every input; otherwise a run whose
@@ -104,14 +105,22 @@ __device__ __forceinline__ void wave_max_publish(double v, unsigned long long *w
   for (int off = 32; off; off >>= 1) v = fmax(v, __shfl_xor(v, off));
   if ((threadIdx.x & 63) == 0) atomicMax(word, (unsigned long long)__double_as_longlong(v));
 }
-__global__ __launch_bounds__(256) void max_abs_kernel(const double2 *__restrict__ x, size_t n,
-                                                      unsigned long long *word) {
+// Largest |K^| of each stored key-spectrum row (len complex values; one workgroup per row):
+// kappa_r of the a priori bound, rounded up past sqrt's error.
+__global__ __launch_bounds__(256) void row_max_abs_kernel(const double2 *__restrict__ x, int len,
+                                                          double *__restrict__ out) {
+  __shared__ double wm[4];
+  const double2 *row = x + (size_t)blockIdx.x * len;
   double m = 0.0;
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
-    const double2 v = x[i];
-    m = fmax(m, sqrt(v.x * v.x + v.y * v.y) * (1.0 + 0x1p-50));  // rounded up past sqrt's error
+  for (int i = threadIdx.x; i < len; i += 256) {
+    const double2 v = row[i];
+    m = fmax(m, sqrt(v.x * v.x + v.y * v.y) * (1.0 + 0x1p-50));
   }
-  wave_max_publish(m, word);
+#pragma unroll
+  for (int off = 32; off; off >>= 1) m = fmax(m, __shfl_xor(m, off));
+  if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) out[blockIdx.x] = fmax(fmax(wm[0], wm[1]), fmax(wm[2], wm[3]));
 }
 
 // ---- rounding-margin guard ----------------------------------------------------------------------
