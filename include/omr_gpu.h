@@ -194,6 +194,9 @@ omr_status omr_ctx_rounding_margin(omr_ctx *ctx, double observed[2], double apri
  * of level 1 (BSK1, [512][8][2][512], /512) or level 2 (BSK2 limbs, [670][12][2][2][1024], /1024),
  * in the kernels' storage order (register-major slots). */
 omr_status omr_ctx_key_spectrum(omr_ctx *ctx, int level, size_t first, size_t count, double *out);
+/* Diagnostics (host only, no GPU): the double-double twiddles of the key transform of `level`
+ * (n - 1 entries, stage s node i at (1 << s) - 1 + i; per entry re.hi, re.lo, im.hi, im.lo). */
+omr_status omr_fft_twiddles_dd(int level, double *out);
 /* Encode workgroups fold ceil(D / max_chunks) messages each (at least 32, or 128 from D = 16,384),
  * so a call keeps at most `max_chunks` partial digests per ciphertext (32 KiB each); 0 = the
  * default 4,096. A memory knob: the digests are identical for every setting. */

@@ -145,6 +145,7 @@ pub mod ffi {
         pub fn omr_ctx_set_rounding_guard(ctx: *mut OmrCtx, enable: c_int) -> OmrStatus;
         pub fn omr_ctx_rounding_margin(ctx: *mut OmrCtx, observed: *mut f64, apriori: *mut f64, kappa: *mut f64,
                                        reset: c_int) -> OmrStatus;
+        pub fn omr_fft_twiddles_dd(level: c_int, out: *mut f64) -> OmrStatus;
         pub fn omr_ctx_key_spectrum(ctx: *mut OmrCtx, level: c_int, first: usize, count: usize,
                                     out: *mut f64) -> OmrStatus;
         pub fn omr_encode_indices(ctx: *mut OmrCtx, pv: *const u64, d: usize, global_offset: usize,

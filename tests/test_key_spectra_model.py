@@ -79,3 +79,116 @@ def test_apriori_bound_proves_both_levels_exact_on_the_bench_key():
     e1, e2, k1, k2 = apriori_bounds(PL.keys()[2])
     assert e1 < 0.15 and e2 < 0.45, (e1, e2)
     assert 5e6 < k1 < 2e7 and 1e6 < k2 < 3e6  # ~4 sigma of uniform keys' spectra
+
+
+def test_double_double_twiddles_match_long_double():
+    """The library's double-double twiddles (host code of the key transform, no GPU) equal
+    exp(i pi h / 2n) of the tree (eps recursion) to within long double's own accuracy, and each
+    double-double is normalised (|lo| <= ulp(hi) / 2)."""
+    import product_lib as PL
+    A = PL.omr_amd
+    pi = np.arctan(np.longdouble(1)) * 4
+    for level, L in ((1, 9), (2, 10)):
+        n = 1 << L
+        tw = A.fft_twiddles_dd(level)
+        half, eps = [], [n]
+        for s in range(L):
+            half += [e // 2 for e in eps]
+            eps = [y for e in eps for y in ((e // 2) % (4 * n), (e // 2 + 2 * n) % (4 * n))]
+        ang = pi * np.array(np.array(half) % (4 * n), dtype=np.longdouble) / np.longdouble(2 * n)
+        re = tw[:, 0].astype(np.longdouble) + tw[:, 1].astype(np.longdouble)
+        im = tw[:, 2].astype(np.longdouble) + tw[:, 3].astype(np.longdouble)
+        assert np.max(np.abs(re - np.cos(ang))) < 2e-18 and np.max(np.abs(im - np.sin(ang))) < 2e-18
+        for c in (0, 2):
+            assert np.all(np.abs(tw[:, c + 1]) <= np.spacing(np.abs(tw[:, c])) / 2 + 1e-300)
+
+
+def _dd_two_sum(a, b):
+    s = a + b
+    bb = s - a
+    return s, (a - (s - bb)) + (b - bb)
+
+
+def _dd_quick(a, b):
+    s = a + b
+    return s, b - (s - a)
+
+
+def _dd_add(ah, al, bh, bl):
+    sh, sl = _dd_two_sum(ah, bh)
+    th, tl = _dd_two_sum(al, bl)
+    sl = sl + th
+    sh, sl = _dd_quick(sh, sl)
+    sl = sl + tl
+    return _dd_quick(sh, sl)
+
+
+def _two_prod(a, b):
+    p = a * b
+    # Dekker split (no fma in numpy): exact error of the product
+    c = 134217729.0
+    def split(x):
+        t = c * x
+        hi = t - (t - x)
+        return hi, x - hi
+    ah, al = split(a)
+    bh, bl = split(b)
+    return p, ((ah * bh - p) + ah * bl + al * bh) + al * bl
+
+
+def _dd_mul(ah, al, bh, bl):
+    p, e = _two_prod(ah, bh)
+    e = e + (ah * bl + al * bh)
+    return _dd_quick(p, e)
+
+
+def test_double_double_tree_meets_the_storage_bound():
+    """key_spectrum_dd_kernel's arithmetic (exactness.hpp dd_add / dd_mul, the tree of dd_tree_fft)
+    replayed in numpy float64 on key-sized rows with the library's twiddles: rounded once, every
+    spectral value is within u |K| (1 + 2^-10) of a long-double evaluation -- the storage term
+    u' = u (1 + 2^-40) of the a priori bound up to the reference's own accuracy."""
+    import product_lib as PL
+    A = PL.omr_amd
+    rng = np.random.default_rng(5)
+    pi = np.arctan(np.longdouble(1)) * 4
+    for level, L, lim in ((1, 9, 2 ** 26), (2, 10, 2 ** 24)):
+        n = 1 << L
+        tw = A.fft_twiddles_dd(level)
+        z = rng.integers(-lim, lim, (4, 2 * n)).astype(np.float64)
+        rh, ih = z[:, :n].copy(), z[:, n:].copy()
+        rl, il = np.zeros_like(rh), np.zeros_like(ih)
+        for s in range(L):
+            h = 1 << (L - 1 - s)
+            blk = np.arange(n // 2) >> (L - 1 - s)
+            j = (blk << (L - s)) | (np.arange(n // 2) & (h - 1))
+            j1 = j + h
+            w = tw[(1 << s) - 1 + blk]
+            # v = w * x1 (complex double-double)
+            a1 = _dd_mul(w[:, 0], w[:, 1], rh[:, j1], rl[:, j1])
+            a2 = _dd_mul(w[:, 2], w[:, 3], ih[:, j1], il[:, j1])
+            vr = _dd_add(a1[0], a1[1], -a2[0], -a2[1])
+            b1 = _dd_mul(w[:, 0], w[:, 1], ih[:, j1], il[:, j1])
+            b2 = _dd_mul(w[:, 2], w[:, 3], rh[:, j1], rl[:, j1])
+            vi = _dd_add(b1[0], b1[1], b2[0], b2[1])
+            x0 = (rh[:, j].copy(), rl[:, j].copy(), ih[:, j].copy(), il[:, j].copy())
+            rh[:, j], rl[:, j] = _dd_add(x0[0], x0[1], vr[0], vr[1])
+            ih[:, j], il[:, j] = _dd_add(x0[2], x0[3], vi[0], vi[1])
+            rh[:, j1], rl[:, j1] = _dd_add(x0[0], x0[1], -vr[0], -vr[1])
+            ih[:, j1], il[:, j1] = _dd_add(x0[2], x0[3], -vi[0], -vi[1])
+        # long-double reference of the same tree (twiddles from the eps recursion)
+        x = (z[:, :n] + 1j * z[:, n:]).astype(np.clongdouble)
+        eps = [n]
+        for s in range(L):
+            h = 1 << (L - 1 - s)
+            half = np.array([e // 2 for e in eps])
+            ang = pi * np.array(half % (4 * n), dtype=np.longdouble) / np.longdouble(2 * n)
+            wv = np.cos(ang) + 1j * np.sin(ang)
+            xv = x.reshape(4, 1 << s, 2, h)
+            v = wv[None, :, None] * xv[:, :, 1, :]
+            a, b = xv[:, :, 0, :] + v, xv[:, :, 0, :] - v
+            xv[:, :, 0, :], xv[:, :, 1, :] = a, b
+            eps = [y for e in eps for y in ((e // 2) % (4 * n), (e // 2 + 2 * n) % (4 * n))]
+        K = x / n
+        got = (rh + 1j * ih).astype(np.clongdouble) / n
+        err = np.abs(got - K)
+        assert np.all(err <= 2.0 ** -53 * np.abs(K) * (1 + 2 ** -10) + 1e-17 * np.abs(K).max()), (level, err.max())

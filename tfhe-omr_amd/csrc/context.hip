@@ -888,6 +888,18 @@ extern "C" omr_status omr_ctx_rounding_margin(omr_ctx *c, double observed[2], do
   return OMR_OK;
 }
 
+extern "C" omr_status omr_fft_twiddles_dd(int level, double *out) {
+  if ((level != 1 && level != 2) || !out) return set_error(OMR_ERR_INVALID_ARGUMENT, "omr_fft_twiddles_dd: bad argument");
+  const auto tw = dd_tree_twiddles(level == 1 ? 9 : 10);
+  for (size_t i = 0; i < tw.size(); ++i) {
+    out[4 * i] = tw[i].re.hi;
+    out[4 * i + 1] = tw[i].re.lo;
+    out[4 * i + 2] = tw[i].im.hi;
+    out[4 * i + 3] = tw[i].im.lo;
+  }
+  return OMR_OK;
+}
+
 extern "C" omr_status omr_ctx_key_spectrum(omr_ctx *c, int level, size_t first, size_t count, double *out) {
   const size_t total = level == 1 ? BSK1_ELEMS / 2 : BSK2_ELEMS;  // double2 values
   if (!c || !out || (level != 1 && level != 2) || first > total || count > total - first)

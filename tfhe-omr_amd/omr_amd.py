@@ -85,6 +85,7 @@ EXPORTS = {
     "omr_ctx_check": (C.c_int, [C.c_void_p, C.c_void_p]),
     "omr_ctx_set_rounding_guard": (C.c_int, [C.c_void_p, C.c_int]),
     "omr_ctx_rounding_margin": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]),
+    "omr_fft_twiddles_dd": (C.c_int, [C.c_int, np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS")]),
     "omr_ctx_key_spectrum": (C.c_int, [C.c_void_p, C.c_int, C.c_size_t, C.c_size_t,
                                        np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS")]),
     "omr_encode_indices": (C.c_int, [C.c_void_p, _u64p, C.c_size_t, C.c_size_t, C.c_size_t, C.c_uint64,
@@ -306,6 +307,14 @@ def save_ciphertexts(path: str, cts) -> None:
 
 def load_ciphertexts(path: str) -> np.ndarray:
     return np.array(read_arrays(path, KIND_CIPHERTEXTS)[0])
+
+
+def fft_twiddles_dd(level: int) -> np.ndarray:
+    """The key transform's double-double twiddles [n - 1][4] (re.hi, re.lo, im.hi, im.lo)."""
+    n = 512 if level == 1 else 1024
+    out = np.zeros(4 * (n - 1), dtype=np.float64)
+    _check(lib().omr_fft_twiddles_dd(int(level), out), "omr_fft_twiddles_dd")
+    return out.reshape(n - 1, 4)
 
 
 def detect_kernels() -> dict:
