@@ -73,6 +73,103 @@ __global__ __launch_bounds__(256) void bsk1_latency_layout_kernel(const double2 
   out[idx] = in[((i * 8 + r) * 2 + o) * 512 + key1_pos(lane, e)];
 }
 
+#ifndef OMR_BR1L_SPLIT
+#define OMR_BR1L_SPLIT 0
+#endif
+// Split level-1 inverse (OMR_BR1L_SPLIT): two waves per output. Both read the output spectrum (P3
+// order), apply inverse stage 8 (index bit 0) with WgFft::inv2, and wave g keeps the 4 registers
+// with index bit 0 == g, a 256-point half that stages 7..0 never mix with the other half: radix-4
+// inverse passes (stages 7/6, 5/4, 3/2, 1/0) on layouts H0 -> H3 with a wave-local LDS exchange, a
+// permlane relayout and another wave-local exchange (tests/test_br1l_split_layout.py). H3 holds
+// point g + 2 l + 128 f on lane l, register f: the real part is coefficient j, the imaginary part
+// coefficient j + 512 of the folded polynomial. 4 waves (one per SIMD) share the inverses that
+// waves 0 / 1 ran alone.
+struct HalfInv1 {
+  static constexpr int TW_OFF6 = 0, TW_OFF4 = 192, TW_OFF2 = 240, TW_OFF0 = 252, TW_LEN = 255;
+  OMR_HD static constexpr int jh(int p, int g, int l, int f) {
+    const int f0 = f & 1, f1 = (f >> 1) & 1;
+    const int l0 = l & 1, l1 = (l >> 1) & 1, l2 = (l >> 2) & 1, l3 = (l >> 3) & 1, l4 = (l >> 4) & 1, l5 = (l >> 5) & 1;
+    return g | (p == 0 ? (f0 << 1) | (f1 << 2) | (l5 << 3) | (l0 << 4) | (l1 << 5) | (l2 << 6) | (l3 << 7) | (l4 << 8)
+              : p == 1 ? (f0 << 3) | (f1 << 4) | (l4 << 5) | (l5 << 6) | (l0 << 1) | (l1 << 2) | (l2 << 7) | (l3 << 8)
+              : p == 2 ? (f0 << 5) | (f1 << 6) | (l4 << 3) | (l5 << 4) | (l0 << 1) | (l1 << 2) | (l2 << 7) | (l3 << 8)
+                       : (l << 1) | (f << 7));
+  }
+  // LDS slots of the two wave-local exchanges (k = index >> 1): writes conflict free, reads at
+  // most 2-way (tests/test_br1l_split_layout.py models the banks)
+  OMR_HD static constexpr int slot01(int j) {
+    const int k = j >> 1;
+    return k ^ ((k >> 3) & 1) ^ (((k >> 4) & 1) << 2) ^ (((k >> 5) & 1) << 1);
+  }
+  OMR_HD static constexpr int slot23(int j) {
+    const int k = j >> 1;
+    return k ^ ((k >> 1) & 1) ^ (((k >> 6) & 1) << 2);
+  }
+  __device__ static __forceinline__ void cmulc(double &xr, double &xi, double2 w) {  // * conj(w)
+    const double r = __fma_rn(xr, w.x, xi * w.y);
+    const double i = __fma_rn(xi, w.x, -xr * w.y);
+    xr = r;
+    xi = i;
+  }
+  // inverse radix-4 block on pass stage S (stages S + 1, S): the adjoint network of the forward
+  // block (a0 + a1, a0 - a1, b0 + i b1, b0 - i b1), then * conj(1, B, A, AB)
+  template <int S>
+  __device__ static __forceinline__ void inv_pass(double (&xr)[4], double (&xi)[4], const double2 *tw, int node) {
+    const double a0r = xr[0] + xr[1], a0i = xi[0] + xi[1], a1r = xr[0] - xr[1], a1i = xi[0] - xi[1];
+    const double b0r = xr[2] + xr[3], b0i = xi[2] + xi[3];
+    const double b1r = xi[2] - xi[3], b1i = xr[3] - xr[2];  // -i (o2 - o3)
+    xr[0] = a0r + b0r;
+    xi[0] = a0i + b0i;
+    xr[2] = a0r - b0r;
+    xi[2] = a0i - b0i;
+    xr[1] = a1r + b1r;
+    xi[1] = a1i + b1i;
+    xr[3] = a1r - b1r;
+    xi[3] = a1i - b1i;
+    const int off = (S == 6 ? TW_OFF6 : S == 4 ? TW_OFF4 : S == 2 ? TW_OFF2 : TW_OFF0) + 3 * node;
+    cmulc(xr[1], xi[1], tw[off]);      // B
+    cmulc(xr[2], xi[2], tw[off + 1]);  // A
+    cmulc(xr[3], xi[3], tw[off + 2]);  // AB
+  }
+  __device__ static __forceinline__ void perm(double (&xr)[4], double (&xi)[4]) {
+    swap_lane_bit<4>(xr[0], xr[1]);
+    swap_lane_bit<4>(xi[0], xi[1]);
+    swap_lane_bit<4>(xr[2], xr[3]);
+    swap_lane_bit<4>(xi[2], xi[3]);
+    swap_lane_bit<5>(xr[0], xr[2]);
+    swap_lane_bit<5>(xi[0], xi[2]);
+    swap_lane_bit<5>(xr[1], xr[3]);
+    swap_lane_bit<5>(xi[1], xi[3]);
+  }
+  template <int PF, int PT, bool S01>
+  __device__ static __forceinline__ void exchange(double (&xr)[4], double (&xi)[4], double2 *buf, int g, int l) {
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      const int j = jh(PF, g, l, f);
+      buf[S01 ? slot01(j) : slot23(j)] = make_double2(xr[f], xi[f]);
+    }
+    wave_lds_sync();
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      const int j = jh(PT, g, l, f);
+      const double2 v = buf[S01 ? slot01(j) : slot23(j)];
+      xr[f] = v.x;
+      xi[f] = v.y;
+    }
+    wave_lds_fence();
+  }
+  // stages 7..0 of half g from H0 (registers after stage 8) to H3; buf: the wave's 256-slot area
+  __device__ static __forceinline__ void inv(double (&xr)[4], double (&xi)[4], double2 *buf, const double2 *tw, int g,
+                                             int l) {
+    inv_pass<6>(xr, xi, tw, jh(0, g, l, 0) >> 3);
+    exchange<0, 1, true>(xr, xi, buf, g, l);
+    inv_pass<4>(xr, xi, tw, jh(1, g, l, 0) >> 5);
+    perm(xr, xi);
+    inv_pass<2>(xr, xi, tw, jh(2, g, l, 0) >> 7);
+    exchange<2, 3, false>(xr, xi, buf, g, l);
+    inv_pass<0>(xr, xi, tw, 0);
+  }
+};
+
 template <bool G>
 __device__ __forceinline__ void br1l_body(
     const uint16_t *__restrict__ clue_a, const uint16_t *__restrict__ clue_b,
@@ -103,9 +200,28 @@ __device__ __forceinline__ void br1l_body(
     for (int i = threadIdx.x; i < N0; i += 64 * W) la[i] = lwe_a[g * N0 + i] & (Q0 - 1);
     b = lwe_b[g] & (Q0 - 1);
   }
+  const int r0 = (2 * N1 - (b % (2 * N1))) % (2 * N1);
+#if OMR_BR1L_SPLIT
+  // ACC = (0, X^{-b} * LUT1): waves 0 / 2 own the mask accumulator, waves 1 / 3 the body, wave
+  // 2h + o the coefficients of half h (HalfInv1: point g + 2 l + 128 f, coefficients j, j + 512)
+  __shared__ double2 twh[HalfInv1::TW_LEN];
+  const int own_o = wave & 1, own_g = (wave >> 1) & 1;
+  int ac[8];
+#pragma unroll
+  for (int f = 0; f < 4; ++f)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int c = HalfInv1::jh(3, own_g, lane, f) + 512 * h;
+      ac[f + 4 * h] = own_o == 1 ? (int)canon_small<Mod<1>>(rot_read<N1>(tb.lut1, c, r0)) : 0;
+      if (wave < 4) {
+        ext[own_o][c] = ac[f + 4 * h];
+        ext[own_o][N1 + c] = -ac[f + 4 * h];
+      }
+    }
+  for (int j = threadIdx.x; j < HalfInv1::TW_LEN; j += 64 * W) twh[j] = tb.fft1h[j];
+#else
   // ACC = (0, X^{-b} * LUT1): wave 0 owns the mask accumulator, wave 1 the body accumulator
   int ac[16];
-  const int r0 = (2 * N1 - (b % (2 * N1))) % (2 * N1);
 #pragma unroll
   for (int i = 0; i < 16; ++i)
     ac[i] = wave == 1 ? (int)canon_small<Mod<1>>(rot_read<N1>(tb.lut1, acc_coef(lane, i), r0)) : 0;
@@ -116,6 +232,7 @@ __device__ __forceinline__ void br1l_body(
       ext[wave][N1 + acc_coef(lane, i)] = -ac[i];
     }
   }
+#endif
   for (int j = threadIdx.x; j < NF; j += 64 * W) tws[j] = tb.fft1[j];
   __syncthreads();
   // Wave v's key slice of an executed step: rows 0..7, outputs A / B at register slot v of every
@@ -186,6 +303,36 @@ __device__ __forceinline__ void br1l_body(
     // while waves 0 / 1 run the inverses (issuing 16 KB per wave before the barrier above held
     // every wave there ~2,300 cycles)
     if (wave >= 2) load_slice(kk, inext2);
+#if OMR_BR1L_SPLIT
+    if (wave < 4) {  // waves 0 / 2: output A (mask), 1 / 3: output B (body), half own_g each
+      double sr[1][8], si[1][8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const double2 v = outs[own_o][e * 64 + lane];
+        sr[0][e] = v.x;
+        si[0][e] = v.y;
+      }
+      F::inv2<1>(sr, si, tws, lane);  // stage 8 (index bit 0: register bit 2 in P3)
+      double hr[4], hi[4];
+#pragma unroll
+      for (int f = 0; f < 4; ++f) {
+        hr[f] = own_g ? sr[0][4 + f] : sr[0][f];
+        hi[f] = own_g ? si[0][4 + f] : si[0][f];
+      }
+      HalfInv1::inv(hr, hi, xch, twh, own_g, lane);
+#pragma unroll
+      for (int f = 0; f < 4; ++f)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const double y = h ? hi[f] : hr[f], v = rint(y);  // exact (< 2^43)
+          rg.note(y, v);
+          const int c = HalfInv1::jh(3, own_g, lane, f) + 512 * h;
+          ac[f + 4 * h] = Lvl1Int::canon(ac[f + 4 * h] + (int)red<Mod<1>>(v));
+          ext[own_o][c] = ac[f + 4 * h];
+          ext[own_o][N1 + c] = -ac[f + 4 * h];
+        }
+    }
+#else
     if (wave < 2) {  // wave 0: output A (mask accumulator), wave 1: output B (body accumulator)
       double sr[1][8], si[1][8];
 #pragma unroll
@@ -206,6 +353,7 @@ __device__ __forceinline__ void br1l_body(
         ext[wave][N1 + acc_coef(lane, q)] = -ac[q];
       }
     }
+#endif
     wg_barrier_lds();  // ACC staged for the next step's digits
     OMR_PHASE(pslot, hs, 7);
     ++hs;
