@@ -339,7 +339,7 @@ def main():
                  "certified": all(o < 1 - e for o, e in zip(rm["observed"], rm["apriori"])),
                  "guarded_output_identical": bool(torch.equal(d_guard, d_out)),
                  "note": "level 1, level 2: largest |y - rint(y)| over every rounded FFT product coefficient "
-                         "of one untimed guarded pass; exact when observed < 1 - apriori (DESIGN.md §3)"}
+                         "of one untimed guarded pass; exact when observed < 1 - apriori (DESIGN.md §3a)"}
     del d_guard
 
     # correctness spot check on this rank's data: the client decrypts (library Retriever, CPU)
