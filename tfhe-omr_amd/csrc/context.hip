@@ -703,7 +703,11 @@ extern "C" omr_status omr_ctx_create(const omr_detection_key_view *key, int devi
   {
     int coop = 0;
     HIP_TRY(hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, device));
-    c->coop = coop != 0;
+    // OMR_COOPERATIVE=0: never use the cooperative multi-CU latency kernels (br2l_kernel and
+    // trace_kernel run instead, bit-identical); see DESIGN.md §5a on the exit-time fault of
+    // processes that made cooperative launches under rocprofv3
+    const char *env = getenv("OMR_COOPERATIVE");
+    c->coop = coop != 0 && !(env && env[0] == '0');
   }
   auto fail = [&](omr_status st) {
     omr_ctx_destroy(c);
