@@ -188,10 +188,12 @@ class SecretKeyPack:
         _check(lib().omr_keygen_secret(seed, C.byref(h)), "omr_keygen_secret")
         self._h = h
         self.seed = seed
+        # bound now: at interpreter shutdown the module's globals (lib) may already be None
+        self._destroy = lib().omr_secret_destroy
 
     def __del__(self):
         if getattr(self, "_h", None):
-            lib().omr_secret_destroy(self._h)
+            self._destroy(self._h)
             self._h = None
 
     def export(self):
@@ -369,6 +371,13 @@ class Retriever:
 # Contexts still open at interpreter exit are destroyed by an atexit hook, which runs before the
 # HIP runtime's own exit-time teardown (a context freed after it faults, e.g. under rocprofv3).
 _LIVE_DETECTORS: "weakref.WeakSet[Detector]" = weakref.WeakSet()
+_destroy_ctx = None  # omr_ctx_destroy, bound by the first Detector (usable at interpreter shutdown)
+
+
+def _bind_destroy():
+    global _destroy_ctx
+    if _destroy_ctx is None:
+        _destroy_ctx = lib().omr_ctx_destroy
 
 
 @atexit.register
@@ -391,6 +400,7 @@ class Detector:
         _check(lib().omr_ctx_create(C.byref(view), device, C.byref(h)), "omr_ctx_create")
         self._h = h
         self.device = device
+        _bind_destroy()
         _LIVE_DETECTORS.add(self)
 
     @classmethod
@@ -403,12 +413,13 @@ class Detector:
         _check(lib().omr_ctx_create(C.byref(view), device, C.byref(h)), "omr_ctx_create")
         self._h = h
         self.device = device
+        _bind_destroy()
         _LIVE_DETECTORS.add(self)
         return self
 
     def close(self):
         if getattr(self, "_h", None):
-            lib().omr_ctx_destroy(self._h)
+            (_destroy_ctx or lib().omr_ctx_destroy)(self._h)
             self._h = None
 
     def __del__(self):
