@@ -26,10 +26,6 @@
 
 #include "latency_kernels.hpp"
 
-#ifndef OMR_BR2F_INV3
-#define OMR_BR2F_INV3 0
-#endif
-
 namespace omr {
 
 struct Fft1024 {
@@ -234,46 +230,6 @@ struct Fft1024 {
     exchange<3, 4, 2, false>(xr, xi, W, t);
     fwd_pass<4>(xr, xi, tws, t);
   }
-  // two unscaled inverses sharing the cross-wave barrier: the wave-local exchanges one after the
-  // other through W, the cross-wave ones through Xa / Xb written together before one barrier
-  __device__ static __forceinline__ void inv2(double (&ar)[E], double (&ai)[E], double (&br)[E], double (&bi)[E],
-                                              double2 *Xa, double2 *Xbuf, double2 *W, const double2 *tws, int t) {
-    inv_pass<4>(ar, ai, tws, t);
-    inv_pass<4>(br, bi, tws, t);
-    exchange<4, 3, 3, false>(ar, ai, W, t);
-    exchange<4, 3, 3, false>(br, bi, W, t);
-    inv_pass<3>(ar, ai, tws, t);
-    inv_pass<3>(br, bi, tws, t);
-    perm(ar, ai);
-    perm(br, bi);
-    inv_pass<2>(ar, ai, tws, t);
-    inv_pass<2>(br, bi, tws, t);
-    {
-      const int bw = swz(1, idx(2, t, 0)), bq = swz(1, idx(1, t, 0));
-#pragma unroll
-      for (int e = 0; e < E; ++e) {
-        Xa[slot_of<1, 2>(bw, e)] = make_double2(ar[e], ai[e]);
-        Xbuf[slot_of<1, 2>(bw, e)] = make_double2(br[e], bi[e]);
-      }
-      wg_barrier_lds();
-#pragma unroll
-      for (int e = 0; e < E; ++e) {
-        const double2 va = Xa[slot_of<1, 1>(bq, e)], vb = Xbuf[slot_of<1, 1>(bq, e)];
-        ar[e] = va.x;
-        ai[e] = va.y;
-        br[e] = vb.x;
-        bi[e] = vb.y;
-      }
-      __builtin_amdgcn_wave_barrier();
-      __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    }
-    inv_pass<1>(ar, ai, tws, t);
-    inv_pass<1>(br, bi, tws, t);
-    perm(ar, ai);
-    perm(br, bi);
-    inv_pass<0>(ar, ai, tws, t);
-    inv_pass<0>(br, bi, tws, t);
-  }
   // unscaled inverse (x 1024; the keys carry 1/1024): in P4 layout, out P0 layout
   __device__ static __forceinline__ void inv(double (&xr)[E], double (&xi)[E], double2 *X, double2 *W,
                                              const double2 *tws, int t) {
@@ -324,13 +280,7 @@ __device__ __forceinline__ void br2f_body(const uint32_t *__restrict__ lwe_int, 
   constexpr int E = F::E, NN = N2;
   static_assert(F::TW_LEN <= F::n, "the twiddle table's LDS doubles as the trace's NTT table");
   __shared__ double2 tws[F::n];
-#if OMR_BR2F_INV3
-  // X0, X1, W, X2 (80 KB per workgroup with the twiddles: still two workgroups per CU)
-  __shared__ double2 lds2[4][F::n];
-  double2 *X2 = lds2[3];
-#else
   __shared__ double2 lds2[3][F::n];  // X0, X1, W; the trace's 3 N2 doubles afterwards
-#endif
   double2(&Xb)[2][F::n] = *reinterpret_cast<double2(*)[2][F::n]>(&lds2[0][0]);
   double2 *W = lds2[2];
   const int t = threadIdx.x;
@@ -381,11 +331,7 @@ __device__ __forceinline__ void br2f_body(const uint32_t *__restrict__ lwe_int, 
     for (int p = 0; p < 2; ++p) {
       uint32_t pk[2][E][DG::DW];  // [coefficient j / j + 1024][point] digit words
       {  // digits of (X^a - 1) * ACC_p, staged in X1 (mask) / X0 (body)
-#if OMR_BR2F_INV3
-        double *st = reinterpret_cast<double *>(p == 0 ? X2 : Xb[0]);  // mask staged in X2 (see the inverses)
-#else
         double *st = reinterpret_cast<double *>(Xb[p == 0 ? 1 : 0]);
-#endif
 #pragma unroll
         for (int h = 0; h < 2; ++h)
 #pragma unroll
@@ -441,24 +387,11 @@ __device__ __forceinline__ void br2f_body(const uint32_t *__restrict__ lwe_int, 
         }
       }
     }
-    // inverses, rounding to the exact limb products, recombination mod q2. OMR_BR2F_INV3: (A, lo)
-    // through X1, then (A, hi) and (B, lo) together through X0 and X2 (one barrier), then (B, hi)
-    // through X1: three barriers instead of four. Every cross-wave use rewrites a buffer whose
-    // readers have passed a later barrier (X0: the last body digit's, X2: this step's mask
-    // staging, X1: the first inverse's), and the next step stages the mask in X2 (its readers,
-    // the pair's, passed the last inverse's barrier).
-#if OMR_BR2F_INV3
-    F::inv(sr[0][0], si[0][0], Xb[1], W, tws, t);
-    F::inv2(sr[0][1], si[0][1], sr[1][0], si[1][0], Xb[0], X2, W, tws, t);
-#endif
+    // inverses (X1, X0, X1, X0), rounding to the exact limb products, recombination mod q2
 #pragma unroll
     for (int o = 0; o < 2; ++o) {
-#if OMR_BR2F_INV3
-      if (o == 1) F::inv(sr[1][1], si[1][1], Xb[1], W, tws, t);
-#else
 #pragma unroll
       for (int l = 0; l < 2; ++l) F::inv(sr[o][l], si[o][l], Xb[1 - l], W, tws, t);
-#endif
 #pragma unroll
       for (int e = 0; e < E; ++e)
 #pragma unroll

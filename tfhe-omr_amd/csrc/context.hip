@@ -239,43 +239,8 @@ double apriori_bound(int level, const std::vector<double> &kmax) {
   return (double)n * D * worst * (1 + 0x1p-30);
 }
 
-// Split level-1 inverse (latency_kernels.hpp HalfInv1): radix-4 pass stage s in {6, 4, 2, 0} of the
-// n = 512 tree, block hi < 2^s: (B, A, AB) with A = W(s, hi), B = W(s + 1, 2 hi) at off(s) + 3 hi
-std::vector<double2> fft1_half_twiddles() {
-  const int L = 9, n = 1 << L;
-  std::vector<std::vector<long>> half(L);
-  std::vector<long> eps{n};
-  for (int s = 0; s < L; ++s) {
-    std::vector<long> next;
-    for (long e : eps) {
-      half[s].push_back(e / 2);
-      next.push_back((e / 2) % (4 * n));
-      next.push_back((e / 2 + 2 * n) % (4 * n));
-    }
-    eps.swap(next);
-  }
-  auto at = [&](long h) {
-    const long double ang = 3.14159265358979323846264338327950288L * (long double)(h % (8 * n)) / (long double)(2 * n);
-    return make_double2((double)cosl(ang), (double)sinl(ang));
-  };
-  std::vector<double2> tw(HalfInv1::TW_LEN);
-  for (int s : {6, 4, 2, 0}) {
-    const int off = s == 6 ? HalfInv1::TW_OFF6 : s == 4 ? HalfInv1::TW_OFF4 : s == 2 ? HalfInv1::TW_OFF2 : HalfInv1::TW_OFF0;
-    for (int hi = 0; hi < (1 << s); ++hi) {
-      const long a = half[s][hi], b = half[s + 1][2 * hi];
-      tw[off + 3 * hi] = at(b);
-      tw[off + 3 * hi + 1] = at(a);
-      tw[off + 3 * hi + 2] = at(a + b);
-    }
-  }
-  return tw;
-}
-
 }  // namespace
 
-#ifndef OMR_BR2Y
-#define OMR_BR2Y 0
-#endif
 #ifndef OMR_DEFAULT_LATENCY_MAX
 #define OMR_DEFAULT_LATENCY_MAX 64  // chunks up to this many messages run the latency kernels
 #endif
@@ -286,7 +251,6 @@ struct omr_ctx {
   double2 *bsk1f = nullptr;  // level-1 FFT-domain keys [512][8][2][512] complex, x 1/512
   double2 *bsk1l = nullptr;  // the same in br1l_kernel's layout [512][8 slot][8 row][2][64 lane]
   double2 *fft1 = nullptr;   // level-1 FFT twiddles
-  double2 *fft1h = nullptr;  // split level-1 inverse twiddles (HalfInv1)
   double *bsk2 = nullptr, *tk = nullptr;  // BSK2 NTT domain (latency kernels), trace key
   double2 *bsk2f = nullptr;                // BSK2 as FFT-domain 25-bit limbs (br2f_kernel), x 1/1024
   double2 *fft2 = nullptr;                 // Fft1024 twiddles
@@ -587,11 +551,7 @@ omr_status launch_br2x(omr_ctx *c, size_t n, const uint32_t *lwe_int, uint64_t *
   int *err = c->x_err;
   void *args[] = {(void *)&lwe_int, (void *)&bsk2, (void *)&tb, (void *)&slots, (void *)&flags, (void *)&err,
                   (void *)&out};
-#if OMR_BR2Y  // both groups of each CU share the partial combination, hand-off and inverse
-  const void *kern = reinterpret_cast<const void *>(&br2y_kernel);
-#else
   const void *kern = reinterpret_cast<const void *>(&br2x_kernel);
-#endif
   const hipError_t e = hipLaunchCooperativeKernel(kern, dim3((unsigned)(2 * n)), dim3(BR2L_T), args, 0, st);
   if (e == hipErrorCooperativeLaunchTooLarge || e == hipErrorNotSupported || e == hipErrorInvalidConfiguration) {
     (void)hipGetLastError();  // refused: nothing was enqueued
@@ -768,13 +728,6 @@ extern "C" omr_status omr_ctx_create(const omr_detection_key_view *key, int devi
   if (hipMemcpy(c->fft1, ftw.data(), ftw.size() * sizeof(double2), hipMemcpyHostToDevice) != hipSuccess)
     return fail(set_error(OMR_ERR_DEVICE, "omr_ctx_create: table upload"));
   c->tb.fft1 = c->fft1;
-  {
-    const auto fh = fft1_half_twiddles();
-    if (hipMalloc(&c->fft1h, fh.size() * sizeof(double2)) != hipSuccess ||
-        hipMemcpy(c->fft1h, fh.data(), fh.size() * sizeof(double2), hipMemcpyHostToDevice) != hipSuccess)
-      return fail(set_error(OMR_ERR_OUT_OF_MEMORY, "omr_ctx_create: tables"));
-    c->tb.fft1h = c->fft1h;
-  }
   const auto ftw2 = fft2_twiddles();
   if (hipMalloc(&c->fft2, ftw2.size() * sizeof(double2)) != hipSuccess)
     return fail(set_error(OMR_ERR_OUT_OF_MEMORY, "omr_ctx_create: tables"));
@@ -846,7 +799,6 @@ extern "C" void omr_ctx_destroy(omr_ctx *c) {
   dev_free(c->bsk1f);
   dev_free(c->bsk1l);
   dev_free(c->fft1);
-  dev_free(c->fft1h);
   dev_free(c->bsk2);
   dev_free(c->bsk2f);
   dev_free(c->fft2);

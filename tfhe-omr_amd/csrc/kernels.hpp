@@ -23,7 +23,6 @@ struct DeviceTables {
   const uint16_t *trace_perm;             // [11][2048] NTT-domain permutation of sigma_g
   const uint16_t *trace_src;              // [11][2048] coefficient source index of sigma_g (+N: negate)
   const double2 *fft1;                    // level-1 FFT twiddles
-  const double2 *fft1h;                   // split level-1 inverse: (B, A, AB) of its radix-4 blocks
 };
 
 // ---- key conversion: coefficient-domain canonical residues -> NTT-domain centred residues ----

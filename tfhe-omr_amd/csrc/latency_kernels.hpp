@@ -73,103 +73,6 @@ __global__ __launch_bounds__(256) void bsk1_latency_layout_kernel(const double2 
   out[idx] = in[((i * 8 + r) * 2 + o) * 512 + key1_pos(lane, e)];
 }
 
-#ifndef OMR_BR1L_SPLIT
-#define OMR_BR1L_SPLIT 0
-#endif
-// Split level-1 inverse (OMR_BR1L_SPLIT): two waves per output. Both read the output spectrum (P3
-// order), apply inverse stage 8 (index bit 0) with WgFft::inv2, and wave g keeps the 4 registers
-// with index bit 0 == g, a 256-point half that stages 7..0 never mix with the other half: radix-4
-// inverse passes (stages 7/6, 5/4, 3/2, 1/0) on layouts H0 -> H3 with a wave-local LDS exchange, a
-// permlane relayout and another wave-local exchange (tests/test_br1l_split_layout.py). H3 holds
-// point g + 2 l + 128 f on lane l, register f: the real part is coefficient j, the imaginary part
-// coefficient j + 512 of the folded polynomial. 4 waves (one per SIMD) share the inverses that
-// waves 0 / 1 ran alone.
-struct HalfInv1 {
-  static constexpr int TW_OFF6 = 0, TW_OFF4 = 192, TW_OFF2 = 240, TW_OFF0 = 252, TW_LEN = 255;
-  OMR_HD static constexpr int jh(int p, int g, int l, int f) {
-    const int f0 = f & 1, f1 = (f >> 1) & 1;
-    const int l0 = l & 1, l1 = (l >> 1) & 1, l2 = (l >> 2) & 1, l3 = (l >> 3) & 1, l4 = (l >> 4) & 1, l5 = (l >> 5) & 1;
-    return g | (p == 0 ? (f0 << 1) | (f1 << 2) | (l5 << 3) | (l0 << 4) | (l1 << 5) | (l2 << 6) | (l3 << 7) | (l4 << 8)
-              : p == 1 ? (f0 << 3) | (f1 << 4) | (l4 << 5) | (l5 << 6) | (l0 << 1) | (l1 << 2) | (l2 << 7) | (l3 << 8)
-              : p == 2 ? (f0 << 5) | (f1 << 6) | (l4 << 3) | (l5 << 4) | (l0 << 1) | (l1 << 2) | (l2 << 7) | (l3 << 8)
-                       : (l << 1) | (f << 7));
-  }
-  // LDS slots of the two wave-local exchanges (k = index >> 1): writes conflict free, reads at
-  // most 2-way (tests/test_br1l_split_layout.py models the banks)
-  OMR_HD static constexpr int slot01(int j) {
-    const int k = j >> 1;
-    return k ^ ((k >> 3) & 1) ^ (((k >> 4) & 1) << 2) ^ (((k >> 5) & 1) << 1);
-  }
-  OMR_HD static constexpr int slot23(int j) {
-    const int k = j >> 1;
-    return k ^ ((k >> 1) & 1) ^ (((k >> 6) & 1) << 2);
-  }
-  __device__ static __forceinline__ void cmulc(double &xr, double &xi, double2 w) {  // * conj(w)
-    const double r = __fma_rn(xr, w.x, xi * w.y);
-    const double i = __fma_rn(xi, w.x, -xr * w.y);
-    xr = r;
-    xi = i;
-  }
-  // inverse radix-4 block on pass stage S (stages S + 1, S): the adjoint network of the forward
-  // block (a0 + a1, a0 - a1, b0 + i b1, b0 - i b1), then * conj(1, B, A, AB)
-  template <int S>
-  __device__ static __forceinline__ void inv_pass(double (&xr)[4], double (&xi)[4], const double2 *tw, int node) {
-    const double a0r = xr[0] + xr[1], a0i = xi[0] + xi[1], a1r = xr[0] - xr[1], a1i = xi[0] - xi[1];
-    const double b0r = xr[2] + xr[3], b0i = xi[2] + xi[3];
-    const double b1r = xi[2] - xi[3], b1i = xr[3] - xr[2];  // -i (o2 - o3)
-    xr[0] = a0r + b0r;
-    xi[0] = a0i + b0i;
-    xr[2] = a0r - b0r;
-    xi[2] = a0i - b0i;
-    xr[1] = a1r + b1r;
-    xi[1] = a1i + b1i;
-    xr[3] = a1r - b1r;
-    xi[3] = a1i - b1i;
-    const int off = (S == 6 ? TW_OFF6 : S == 4 ? TW_OFF4 : S == 2 ? TW_OFF2 : TW_OFF0) + 3 * node;
-    cmulc(xr[1], xi[1], tw[off]);      // B
-    cmulc(xr[2], xi[2], tw[off + 1]);  // A
-    cmulc(xr[3], xi[3], tw[off + 2]);  // AB
-  }
-  __device__ static __forceinline__ void perm(double (&xr)[4], double (&xi)[4]) {
-    swap_lane_bit<4>(xr[0], xr[1]);
-    swap_lane_bit<4>(xi[0], xi[1]);
-    swap_lane_bit<4>(xr[2], xr[3]);
-    swap_lane_bit<4>(xi[2], xi[3]);
-    swap_lane_bit<5>(xr[0], xr[2]);
-    swap_lane_bit<5>(xi[0], xi[2]);
-    swap_lane_bit<5>(xr[1], xr[3]);
-    swap_lane_bit<5>(xi[1], xi[3]);
-  }
-  template <int PF, int PT, bool S01>
-  __device__ static __forceinline__ void exchange(double (&xr)[4], double (&xi)[4], double2 *buf, int g, int l) {
-#pragma unroll
-    for (int f = 0; f < 4; ++f) {
-      const int j = jh(PF, g, l, f);
-      buf[S01 ? slot01(j) : slot23(j)] = make_double2(xr[f], xi[f]);
-    }
-    wave_lds_sync();
-#pragma unroll
-    for (int f = 0; f < 4; ++f) {
-      const int j = jh(PT, g, l, f);
-      const double2 v = buf[S01 ? slot01(j) : slot23(j)];
-      xr[f] = v.x;
-      xi[f] = v.y;
-    }
-    wave_lds_fence();
-  }
-  // stages 7..0 of half g from H0 (registers after stage 8) to H3; buf: the wave's 256-slot area
-  __device__ static __forceinline__ void inv(double (&xr)[4], double (&xi)[4], double2 *buf, const double2 *tw, int g,
-                                             int l) {
-    inv_pass<6>(xr, xi, tw, jh(0, g, l, 0) >> 3);
-    exchange<0, 1, true>(xr, xi, buf, g, l);
-    inv_pass<4>(xr, xi, tw, jh(1, g, l, 0) >> 5);
-    perm(xr, xi);
-    inv_pass<2>(xr, xi, tw, jh(2, g, l, 0) >> 7);
-    exchange<2, 3, false>(xr, xi, buf, g, l);
-    inv_pass<0>(xr, xi, tw, 0);
-  }
-};
-
 template <bool G>
 __device__ __forceinline__ void br1l_body(
     const uint16_t *__restrict__ clue_a, const uint16_t *__restrict__ clue_b,
@@ -201,25 +104,6 @@ __device__ __forceinline__ void br1l_body(
     b = lwe_b[g] & (Q0 - 1);
   }
   const int r0 = (2 * N1 - (b % (2 * N1))) % (2 * N1);
-#if OMR_BR1L_SPLIT
-  // ACC = (0, X^{-b} * LUT1): waves 0 / 2 own the mask accumulator, waves 1 / 3 the body, wave
-  // 2h + o the coefficients of half h (HalfInv1: point g + 2 l + 128 f, coefficients j, j + 512)
-  __shared__ double2 twh[HalfInv1::TW_LEN];
-  const int own_o = wave & 1, own_g = (wave >> 1) & 1;
-  int ac[8];
-#pragma unroll
-  for (int f = 0; f < 4; ++f)
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int c = HalfInv1::jh(3, own_g, lane, f) + 512 * h;
-      ac[f + 4 * h] = own_o == 1 ? (int)canon_small<Mod<1>>(rot_read<N1>(tb.lut1, c, r0)) : 0;
-      if (wave < 4) {
-        ext[own_o][c] = ac[f + 4 * h];
-        ext[own_o][N1 + c] = -ac[f + 4 * h];
-      }
-    }
-  for (int j = threadIdx.x; j < HalfInv1::TW_LEN; j += 64 * W) twh[j] = tb.fft1h[j];
-#else
   // ACC = (0, X^{-b} * LUT1): wave 0 owns the mask accumulator, wave 1 the body accumulator
   int ac[16];
 #pragma unroll
@@ -232,7 +116,6 @@ __device__ __forceinline__ void br1l_body(
       ext[wave][N1 + acc_coef(lane, i)] = -ac[i];
     }
   }
-#endif
   for (int j = threadIdx.x; j < NF; j += 64 * W) tws[j] = tb.fft1[j];
   __syncthreads();
   // Wave v's key slice of an executed step: rows 0..7, outputs A / B at register slot v of every
@@ -303,36 +186,6 @@ __device__ __forceinline__ void br1l_body(
     // while waves 0 / 1 run the inverses (issuing 16 KB per wave before the barrier above held
     // every wave there ~2,300 cycles)
     if (wave >= 2) load_slice(kk, inext2);
-#if OMR_BR1L_SPLIT
-    if (wave < 4) {  // waves 0 / 2: output A (mask), 1 / 3: output B (body), half own_g each
-      double sr[1][8], si[1][8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const double2 v = outs[own_o][e * 64 + lane];
-        sr[0][e] = v.x;
-        si[0][e] = v.y;
-      }
-      F::inv2<1>(sr, si, tws, lane);  // stage 8 (index bit 0: register bit 2 in P3)
-      double hr[4], hi[4];
-#pragma unroll
-      for (int f = 0; f < 4; ++f) {
-        hr[f] = own_g ? sr[0][4 + f] : sr[0][f];
-        hi[f] = own_g ? si[0][4 + f] : si[0][f];
-      }
-      HalfInv1::inv(hr, hi, xch, twh, own_g, lane);
-#pragma unroll
-      for (int f = 0; f < 4; ++f)
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const double y = h ? hi[f] : hr[f], v = rint(y);  // exact (< 2^43)
-          rg.note(y, v);
-          const int c = HalfInv1::jh(3, own_g, lane, f) + 512 * h;
-          ac[f + 4 * h] = Lvl1Int::canon(ac[f + 4 * h] + (int)red<Mod<1>>(v));
-          ext[own_o][c] = ac[f + 4 * h];
-          ext[own_o][N1 + c] = -ac[f + 4 * h];
-        }
-    }
-#else
     if (wave < 2) {  // wave 0: output A (mask accumulator), wave 1: output B (body accumulator)
       double sr[1][8], si[1][8];
 #pragma unroll
@@ -353,7 +206,6 @@ __device__ __forceinline__ void br1l_body(
         ext[wave][N1 + acc_coef(lane, q)] = -ac[q];
       }
     }
-#endif
     wg_barrier_lds();  // ACC staged for the next step's digits
     OMR_PHASE(pslot, hs, 7);
     ++hs;
@@ -691,245 +543,6 @@ __global__ __launch_bounds__(BR2L_T, 1) void br2x_kernel(const uint32_t *__restr
 #pragma unroll
     for (int e = 0; e < E; ++e) o[t + e * T] = to_u64<M>(acc[e]);
   }
-}
-
-// ---- level 2 over two CUs, the inverse split over both groups (br2y_kernel) -----------------
-// br2x_kernel leaves group 1 idle while group 0 combines the partials, hands off the partner's
-// output and runs the inverse (the last ~25 % of a step). Here both groups do half of that: after
-// its multiply-accumulate each group applies inverse stage 10 (index bit 0, register bit 1 of e in
-// CmuxNtt's P3 layout) to its own partials (linear, so the sums commute with it), and then owns the
-// positions with index bit 0 == g, which stages 9..0 never combine with the other half: it takes
-// the other group's partials for them through LDS, hands off / receives that half of the partner
-// CU's output, and runs stages 9..0 of its 1024-point half on 256 threads x 4 registers
-// (HalfInv). ACC_r is then held split: thread t of group g keeps coefficients 2 t + g + 512 f.
-// tests/test_half_inverse_layout.py restates the layouts and checks the split inverse against the
-// full one with exact integers.
-struct HalfInv {
-  using M = Mod<2>;
-  static constexpr int T = 256, F = 4;
-  // index bit 10 - s of inverse stage s sits on register bit h(s) of every layout below
-  OMR_HD static constexpr int h_of(int s) { return s == 9 ? 2 : s == 8 ? 1 : (s & 1) ? 1 : 2; }
-  // index held by register f of thread t of group g in layout Q<p> (tests/test_half_inverse_layout.py jq)
-  OMR_HD static constexpr int jq(int p, int g, int t, int f) {
-    const int f0 = f & 1, f1 = (f >> 1) & 1;
-    const int t0 = t & 1, t1 = (t >> 1) & 1, t2 = (t >> 2) & 1, t3 = (t >> 3) & 1, t4 = (t >> 4) & 1,
-              t5 = (t >> 5) & 1, t6 = (t >> 6) & 1, t7 = (t >> 7) & 1;
-    const int hi = (t6 << 9) | (t7 << 10);
-    return g | (p == 0 ? (f1 << 1) | (f0 << 2) | (t4 << 3) | (t5 << 4) | ((t & 15) << 5) | hi
-              : p == 1 ? (t5 << 1) | (t4 << 2) | (f0 << 3) | (f1 << 4) | ((t & 15) << 5) | hi
-              : p == 2 ? (t3 << 1) | (t2 << 2) | (t1 << 3) | (t0 << 4) | (f0 << 5) | (f1 << 6) | (t4 << 7) | (t5 << 8) | hi
-              : p == 3 ? (t3 << 1) | (t2 << 2) | (t1 << 3) | (t0 << 4) | (t4 << 5) | (t5 << 6) | (f0 << 7) | (f1 << 8) | hi
-                       : (t << 1) | (f << 9));
-  }
-  // P3 register of half register f of group g (layout Q0 is P3 restricted to e bit 1 == g)
-  OMR_HD static constexpr int e_of(int g, int f) { return (f & 1) | (g << 1) | ((f >> 1) << 2); }
-  // inverse stage S on layout P; tw: the CmuxNtt table in LDS (tw2c: stage 9 read through its
-  // permuted slot, stages <= 8 are the plain mirrored tree)
-  template <int P, int S>
-  __device__ static __forceinline__ void stage(double (&x)[F], const double *tw, int g, int t, int &since_red) {
-    constexpr int h = h_of(S);
-    if (since_red >= M::RED_INV) {
-#pragma unroll
-      for (int f = 0; f < F; ++f) x[f] = red<M>(x[f]);
-      since_red = 0;
-    }
-#pragma unroll
-    for (int f = 0; f < F; ++f) {
-      if (f & h) continue;
-      const int slot = S == 9 ? (2 << 9) - 1 - ((f & 1) * 256 + t) : (2 << S) - 1 - (jq(P, g, t, f) >> (11 - S));
-      const double w = tw[slot];
-      const double u = x[f], v = x[f + h];
-      x[f] = u + v;
-      x[f + h] = mm<M>(v - u, w);
-    }
-    ++since_red;
-  }
-  __device__ static __forceinline__ void perm(double (&x)[F]) {  // register bit 0 <-> lane bit 4, bit 1 <-> lane bit 5
-    swap_lane_bit<4>(x[0], x[1]);
-    swap_lane_bit<4>(x[2], x[3]);
-    swap_lane_bit<5>(x[0], x[2]);
-    swap_lane_bit<5>(x[1], x[3]);
-  }
-  // wave-local Q1 -> Q2 slot of index j within the wave's 256 (k = j >> 1 bits 0..7): conflict
-  // free for the ds_write_b64 16-lane groups of Q1 (k4..k7 vary) and the ds_read_b64 32-lane
-  // groups of Q2 (k0..k3, k6 vary)
-  OMR_HD static constexpr int wslot(int j) {
-    const int k = (j >> 1) & 255;
-    const int b[8] = {(k & 1) ^ ((k >> 4) & 1), ((k >> 1) & 1) ^ ((k >> 5) & 1), ((k >> 2) & 1) ^ ((k >> 6) & 1),
-                      ((k >> 3) & 1) ^ ((k >> 7) & 1), (k >> 6) & 1, (k >> 4) & 1, (k >> 5) & 1, (k >> 7) & 1};
-    int s = 0;
-    for (int i = 0; i < 8; ++i) s |= b[i] << i;
-    return ((j >> 9) << 8) | s;
-  }
-  // stages 9..0 of group g's half: in Q0 (P3 registers e_of(g, f)), out Q4 (coefficient 2 t + g + 512 f).
-  // W: the group's wave-local buffer (1024 doubles), X: its cross-wave buffer (1024 doubles; one
-  // workgroup barrier, both groups reach it together)
-  __device__ static __forceinline__ void inv(double (&x)[F], double *X, double *W, const double *tw, int g, int t) {
-    int sr = 0;
-    stage<0, 9>(x, tw, g, t, sr);
-    stage<0, 8>(x, tw, g, t, sr);
-    perm(x);
-    stage<1, 7>(x, tw, g, t, sr);
-    stage<1, 6>(x, tw, g, t, sr);
-#pragma unroll
-    for (int f = 0; f < F; ++f) W[wslot(jq(1, g, t, f))] = x[f];
-    WgNtt<M, 256, 8>::wave_sync();
-#pragma unroll
-    for (int f = 0; f < F; ++f) x[f] = W[wslot(jq(2, g, t, f))];
-    __builtin_amdgcn_wave_barrier();
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    stage<2, 5>(x, tw, g, t, sr);
-    stage<2, 4>(x, tw, g, t, sr);
-    perm(x);
-    stage<3, 3>(x, tw, g, t, sr);
-    stage<3, 2>(x, tw, g, t, sr);
-#pragma unroll
-    for (int f = 0; f < F; ++f) X[jq(3, g, t, f) >> 1] = x[f];
-    wg_barrier_lds();
-#pragma unroll
-    for (int f = 0; f < F; ++f) x[f] = X[jq(4, g, t, f) >> 1];
-    __builtin_amdgcn_wave_barrier();
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    stage<4, 1>(x, tw, g, t, sr);
-    stage<4, 0>(x, tw, g, t, sr);
-  }
-};
-
-__global__ __launch_bounds__(BR2L_T, 1) void br2y_kernel(const uint32_t *__restrict__ lwe_int,
-                                                         const double *__restrict__ bsk2, DeviceTables tb,
-                                                         double *xg, uint32_t *flags, int *err,
-                                                         uint64_t *__restrict__ out) {
-  using M = Mod<2>;
-  constexpr int T = BR2_T, E = BR2_E, N = N2, F = HalfInv::F;
-  using NTT = CmuxNtt;
-  using DG = Digits2;
-  constexpr int KD = D2 / 2;  // digits per group
-  __shared__ double xbuf[2][NTT::LDS_DOUBLES];
-  __shared__ double part[2][N];  // [output][other half of each group: (1 - g) * 1024 + f * 256 + t]
-  __shared__ double tws[N + 136 * 5];
-  __shared__ int stop;
-  const int m = blockIdx.x >> 1, r = blockIdx.x & 1;
-  const int g = threadIdx.x / T, t = threadIdx.x % T;
-  double *X = xbuf[g];
-  double *ST = xbuf[0] + N;  // the staged accumulator (group 0's X1), written by both groups
-  const double *tw = tws, *t0 = tws + N;
-  const uint32_t *lwe = lwe_int + (size_t)m * (NI + 1);
-  double acc[F];  // ACC_r coefficients 2 t + g + 512 f
-  {
-    const int b = (int)lwe[NI];
-    const int rr = (2 * N - (b % (2 * N))) % (2 * N);
-#pragma unroll
-    for (int f = 0; f < F; ++f) acc[f] = r == 1 ? canon_small<M>(rot_read<N>(tb.lut2, HalfInv::jq(4, g, t, f), rr)) : 0.0;
-    for (int j = threadIdx.x; j < N; j += BR2L_T) tws[j] = tb.tw2c[j];
-    if (threadIdx.x <= 128) {  // table k: d * c_k, d = tid - 64 (c = tw1, tw2, tw1 tw2, tw3, tw1 tw3)
-      const double w1 = tb.tw2[1], w2 = tb.tw2[2], w3 = tb.tw2[3];
-      const double c[5] = {w1, w2, canon<M>(mm<M>(w1, w2)), w3, canon<M>(mm<M>(w1, w3))};
-#pragma unroll
-      for (int k = 0; k < 5; ++k)
-        tws[N + 136 * k + threadIdx.x] = canon<M>(mm<M>((double)((int)threadIdx.x - 64), c[k]));
-    }
-    if (threadIdx.x == 0) stop = 0;
-    __syncthreads();
-  }
-  uint32_t *my_flag = flags + 2 * m + r, *their_flag = flags + 2 * m + (1 - r);
-  uint32_t hc = 0;  // hand-offs so far (executed steps)
-#pragma unroll 1
-  for (int i = 0; i < NI; ++i) {
-    const int a = (int)__builtin_amdgcn_readfirstlane(lwe[i]) & (2 * N - 1);
-    if (a == 0) continue;  // (X^0 - 1) * ACC = 0 (both workgroups of the message skip it)
-    const size_t slot = hc & 1;
-    const double *ggsw = bsk2 + ((size_t)i * 2 * D2 + (size_t)r * D2 + (size_t)g * KD) * 2 * N;
-    uint32_t pk[E][DG::DW];
-    {  // digits of (X^a - 1) * ACC_r: both groups stage their halves, both decompose all of it
-#pragma unroll
-      for (int f = 0; f < F; ++f) ST[HalfInv::jq(4, g, t, f)] = acc[f];
-      __syncthreads();
-#pragma unroll
-      for (int e = 0; e < E; ++e)
-        DG::pack(canon_small<M>(rot_read_lds<N>(ST, t + e * T, a) - ST[t + e * T]), pk[e]);
-      __builtin_amdgcn_wave_barrier();
-      __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    }
-    double accA[E], accB[E];
-#pragma unroll
-    for (int e = 0; e < E; ++e) accA[e] = accB[e] = 0.0;
-    KeyRow<double, E> cur;
-    cur.load(ggsw, N, t * E);
-#pragma unroll
-    for (int h = 0; h < KD; ++h) {  // three digits: X0, X1, X0 (the staging used group 0's X1)
-      const int k = g * KD + h;
-      double x[E];
-      int fd[E];
-#pragma unroll
-      for (int e = 0; e < E; ++e) fd[e] = DG::get_int(pk[e], k) + 64;
-      if ((h & 1) == 0)
-        NTT::template fwd_small<0>(fd, t0, x, X, tw, t, tb.tw2c);
-      else
-        NTT::template fwd_small<1>(fd, t0, x, X, tw, t, tb.tw2c);
-#pragma unroll
-      for (int e = 0; e < E; ++e) {
-        accA[e] += mm<M>(x[e], cur.a[e]);
-        accB[e] += mm<M>(x[e], cur.b[e]);
-      }
-      if (h + 1 < KD) cur.load(ggsw + (size_t)(h + 1) * 2 * N, N, t * E);
-    }
-    // inverse stage 10 on this group's partials (three products on a zero sum: |.| < 5.3q)
-#pragma unroll
-    for (int e = 0; e < E; ++e) {
-      accA[e] = red<M>(accA[e]);
-      accB[e] = red<M>(accB[e]);
-    }
-    {
-      int sr = 0;
-      NTT::template stage<3, 10, true>(accA, tw, t, sr);
-      sr = 0;
-      NTT::template stage<3, 10, true>(accB, tw, t, sr);
-    }
-    // the other group's half of both outputs through LDS (lane-contiguous)
-#pragma unroll
-    for (int f = 0; f < F; ++f) {
-      const int e = HalfInv::e_of(1 - g, f);
-      part[0][(1 - g) * 1024 + f * T + t] = red<M>(accA[e]);
-      part[1][(1 - g) * 1024 + f * T + t] = red<M>(accB[e]);
-    }
-    __syncthreads();
-    double keep[F];
-#pragma unroll
-    for (int f = 0; f < F; ++f) {
-      const int e = HalfInv::e_of(g, f);
-      const double sa = red<M>(red<M>(accA[e]) + part[0][g * 1024 + f * T + t]);
-      const double sb = red<M>(red<M>(accB[e]) + part[1][g * 1024 + f * T + t]);
-      keep[f] = r == 0 ? sa : sb;
-      st_sc1(xg + (((size_t)m * 2 + r) * 2 + slot) * N + g * 1024 + f * T + t, r == 0 ? sb : sa);  // the partner's output
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      __hip_atomic_store(my_flag, hc + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      int n = 0;
-      while (__hip_atomic_load(their_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < hc + 1) {
-        if (++n == BR2X_SPIN) {
-          stop = 1;
-          atomicExch(err, 1);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(2);
-      }
-    }
-    __syncthreads();
-    if (stop) break;
-    double s[F];
-#pragma unroll
-    for (int f = 0; f < F; ++f)
-      s[f] = red<M>(keep[f] + ld_sc1(xg + (((size_t)m * 2 + (1 - r)) * 2 + slot) * N + g * 1024 + f * T + t));
-    HalfInv::inv(s, X, X + 2 * N, tw, g, t);
-#pragma unroll
-    for (int f = 0; f < F; ++f) acc[f] = canon<M>(acc[f] + s[f]);
-    ++hc;
-  }
-  uint64_t *o = out + (size_t)m * 2 * N + (size_t)r * N;
-#pragma unroll
-  for (int f = 0; f < F; ++f) o[HalfInv::jq(4, g, t, f)] = to_u64<M>(acc[f]);
 }
 
 // hom_trace (detector.rs:626-639) in place on blind-rotation outputs (coefficient domain,
