@@ -1,0 +1,119 @@
+"""Integer model of br1f's accumulator representation (tfhe-omr_amd/csrc/br1_fft.hpp, Lvl1Off and
+Lvl1Int::round_mod), in numpy with explicit u32 wrap-around, against the plain definitions:
+
+- ac'' = ac + H/2 (mod Q) in [0, Q); the stored negacyclic half n = H - ac'' (signed u32);
+- the digit word from a rotated entry x'' (either half) and the lane's own n equals
+  Lvl1Int::digits(canon(x - ac)), i.e. the NonPowOf2ApproxSignedBasis digits (logB 5, d 4, drop 7)
+  of the reference's decomposition (detector.rs:553-557 via the level-1 parameters);
+- round_mod(y) in [0, Q] with round_mod(y) = round(y) mod Q, and add(ac'', r) = ac'' + r (mod Q)
+  in [0, Q), for FFT outputs y = integer + e (|y| < 2^43, |e| < 0.1), including the multiples of q.
+"""
+import numpy as np
+
+Q = 134215681
+H = (Q - 1) // 2
+HH = H // 2
+M32 = (1 << 32) - 1
+DROP, LOGB, D = 7, 5, 4
+BIAS = ((1 << (LOGB * (D - 1))) - 1) // ((1 << LOGB) - 1) * (1 << (LOGB - 1))
+
+
+def u32(x):
+    return np.asarray(x, dtype=np.int64) & M32
+
+
+def s32(x):
+    x = u32(x)
+    return np.where(x >= 1 << 31, x - (1 << 32), x)
+
+
+def canon(x):
+    x = np.asarray(x, dtype=np.int64) % Q
+    return np.where(x > H, x - Q, x)
+
+
+def ref_digits(v):  # Lvl1Int::digits on a canonical residue
+    return u32((((v + (1 << (DROP - 1))) >> DROP) + BIAS) ^ BIAS)
+
+
+def digit(w, k):  # Lvl1Int::digit: signed field k
+    w = u32(w)
+    if k < D - 1:
+        f = (w >> (LOGB * k)) & 31
+        return np.where(f >= 16, f - 32, f)
+    return s32(w) >> (LOGB * (D - 1))
+
+
+def enc(v):
+    y = u32(v + HH)
+    return np.minimum(y, u32(y + Q))
+
+
+def dec(a):
+    return canon(s32(a) - HH)
+
+
+def neg(a):
+    return u32(H - a)
+
+
+def off_digits(xs, n):
+    t = u32(xs + n)
+    y = np.minimum(np.minimum(t, u32(t + Q)), u32(t - Q))
+    C = (1 << (DROP - 1)) - H + (BIAS << DROP)
+    return u32((s32(y + C) >> DROP) ^ BIAS)
+
+
+def round_mod(y):
+    k = np.floor(y * (1.0 / Q))
+    r = -k * Q + y  # exact for |y| < 2^43 (the fma of the kernel)
+    s = r + 6755399441055744.0
+    return s.view(np.uint64).astype(np.int64) & M32
+
+
+def add(a, r):
+    s = u32(a + r)
+    return np.minimum(s, u32(s - Q))
+
+
+def test_representation_round_trip():
+    v = np.concatenate([np.arange(-H, -H + 1000), np.arange(-500, 500), np.arange(H - 1000, H + 1),
+                        np.random.default_rng(1).integers(-H, H + 1, 200000)])
+    a = enc(v)
+    assert np.all((a >= 0) & (a < Q))
+    assert np.array_equal(dec(a), v)
+    assert np.array_equal(canon(s32(neg(a)) - HH), canon(-v))  # the stored half is "-ac + H/2"
+
+
+def test_digit_words_match_the_decomposition():
+    rng = np.random.default_rng(2)
+    edge = np.array([-H, -H + 1, -1, 0, 1, H - 1, H, HH, -HH, 63, 64, -64, -65])
+    x = np.concatenate([rng.integers(-H, H + 1, 400000), np.repeat(edge, len(edge))])
+    ac = np.concatenate([rng.integers(-H, H + 1, 400000), np.tile(edge, len(edge))])
+    n = neg(enc(ac))
+    for xs in (enc(x), neg(enc(-x))):  # x read from the first half, or -x's entry in the second
+        got = off_digits(xs, n)
+        want = ref_digits(canon(x - ac))
+        assert np.array_equal(got, want)
+    # and the digits recompose the rounded value (the basis of detector.rs's decomposition)
+    w = ref_digits(canon(x - ac))
+    val = sum(digit(w, k) * (32 ** k) for k in range(D))
+    assert np.array_equal(val, (canon(x - ac) + 64) >> DROP)
+    assert np.all(np.abs(np.stack([digit(w, k) for k in range(D)])) <= 17)
+
+
+def test_round_mod_and_update():
+    rng = np.random.default_rng(3)
+    ints = np.concatenate([rng.integers(-(1 << 43), 1 << 43, 300000),
+                           np.arange(-40, 41) * Q, np.arange(-40, 41) * Q + 1, np.arange(-40, 41) * Q - 1,
+                           np.array([(1 << 43) - 1, -(1 << 43) + 1])])
+    for e in (0.0, 0.0999, -0.0999, 0.03):
+        y = ints.astype(np.float64) + e
+        r = round_mod(y)
+        assert np.all((r >= 0) & (r <= Q))
+        assert np.array_equal(r % Q, ints % Q)
+    a = enc(rng.integers(-H, H + 1, ints.size))
+    r = round_mod(ints.astype(np.float64) - 0.05)
+    got = add(a, r)
+    assert np.all((got >= 0) & (got < Q))
+    assert np.array_equal(dec(got), canon(dec(a) + ints))

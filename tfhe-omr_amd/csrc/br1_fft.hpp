@@ -32,17 +32,19 @@ struct Lvl1Int {
     return (int)y - H;
   }
   __device__ static __forceinline__ uint32_t to_u32(int x) { return (uint32_t)(x < 0 ? x + Q : x); }
-  // y = an integer + e (|y| < 2^43, |e| < 0.01: an FFT product output): round(y) mod q, centred,
-  // as an int. The quotient is rint(y / q) and r = y - kq keeps the fraction; adding 1.5 * 2^52
-  // rounds r to the nearest integer in the low mantissa bits, which are its two's complement
-  // (|round(r)| <= H + 1): one FP64 add instead of rint + conversion.
-  // With a RoundGuard, |r - round(r)| = |y - rint(y)| (r = y - kq is exact) is recorded.
+  // y = an integer + e (|y| < 2^43, |e| < 0.1: an FFT product output): round(y) mod q in [0, q], as
+  // a u32. The quotient is floor(y / q) (as computed: it may exceed the true floor only when y is
+  // within 2^-37 q of a multiple of q, and then r rounds to 0; it may fall one short only when the
+  // rounded result is q), r = y - kq keeps the fraction, and adding 1.5 * 2^52 rounds r to the
+  // nearest integer in the low mantissa bits: one FP64 add instead of rint + conversion. The result
+  // q (= 0 mod q) is allowed: Lvl1Off::add folds it. With a RoundGuard, |r - round(r)| =
+  // |y - rint(y)| (r = y - kq is exact) is recorded.
   template <bool G = false>
-  __device__ static __forceinline__ int round_red(double y, RoundGuard<G> *rg = nullptr) {
-    const double r = __fma_rn(-rint(y * (1.0 / 134215681.0)), 134215681.0, y);
+  __device__ static __forceinline__ uint32_t round_mod(double y, RoundGuard<G> *rg = nullptr) {
+    const double r = __fma_rn(-floor(y * (1.0 / 134215681.0)), 134215681.0, y);
     const double s = r + 6755399441055744.0;
     if constexpr (G) rg->note(r, s - 6755399441055744.0);
-    return (int)(uint32_t)__builtin_bit_cast(uint64_t, s);
+    return (uint32_t)__builtin_bit_cast(uint64_t, s);
   }
   // NonPowOf2ApproxSignedBasis (logB 5, d 4, drop 7) on a canonical residue: y = floor((v + 2^6)
   // / 2^7) has balanced base-32 digits d_k in [-16, 15] (k < 3) and an unbounded top digit; in
@@ -68,27 +70,43 @@ struct Lvl1Int {
   }
 };
 
-// br1f keeps ACC offset by H: ac' = ac + H in [0, Q) (u32). A value y in (-Q, 2Q) is reduced to
-// [0, Q) by one v_min3_u32(y, y + Q, y - Q) (the wrapped operands lose), the digit word of the
-// canonical residue y' - H is ((y' - H + 2^6 + 2^7 DIGIT_BIAS) >> 7) ^ DIGIT_BIAS (the bias folded
-// in before the shift), and the stored negacyclic extension 2H - ac' is again "value + H": 7
-// integer operations per digit word instead of 10, 4 per accumulator update instead of 7.
+// br1f keeps ACC offset by H/2: ac'' in [0, Q) with ac'' = ac + H/2 (mod Q). The stored negacyclic
+// extension n = H - ac'' = -ac + H/2 is then in the same representation (as a signed u32, in
+// [-H, H]) and is also the operand of the digit word: for a rotated entry x'' (either half),
+// t = x'' + n = (x - ac) + H (mod Q) with t in (-Q, 2Q), so one v_min3_u32(t, t + Q, t - Q) (the
+// wrapped operands lose) is canon(x - ac) + H in [0, Q), and the digit word of the canonical
+// residue y - H is ((y - H + 2^6 + 2^7 DIGIT_BIAS) >> 7) ^ DIGIT_BIAS (the bias folded in before
+// the shift): 6 integer operations per digit word. The accumulator update adds a rounded product
+// in [0, Q] (Lvl1Int::round_mod): s in [0, 2Q), min(s, s - Q), 3 operations.
 struct Lvl1Off {
-  static constexpr uint32_t Q = (uint32_t)Lvl1Int::Q, H = (uint32_t)Lvl1Int::H;
+  static constexpr uint32_t Q = (uint32_t)Lvl1Int::Q, H = (uint32_t)Lvl1Int::H, OFF = H / 2;
+  static_assert(H % 2 == 0, "H/2 offset");
   __device__ static __forceinline__ uint32_t fold(uint32_t y, uint32_t yq, uint32_t ymq) {  // y, y + Q, y - Q
     return min(min(y, yq), ymq);
   }
-  // digit word of canon(x - ac) from x' = x + H (stored) and n = 2H - ac' = H - ac
+  // centred value v in [-H, H] -> ac''
+  __device__ static __forceinline__ uint32_t enc(int v) {
+    const uint32_t y = (uint32_t)(v + (int)OFF);
+    return min(y, y + Q);
+  }
+  // ac'' -> centred value in [-H, H]
+  __device__ static __forceinline__ int dec(uint32_t acpp) { return Lvl1Int::canon((int)acpp - (int)OFF); }
+  // the stored negacyclic half "-ac + H/2" and the digit operand
+  __device__ static __forceinline__ uint32_t neg(uint32_t acpp) { return H - acpp; }
+  // digit word of canon(x - ac) from a stored entry x'' and n = neg(ac''): t = x - ac + H
   __device__ static __forceinline__ uint32_t digits(uint32_t xs, uint32_t n) {
-    const uint32_t y = fold(xs + n - H, xs + n + (Q - H), xs + n - (Q + H));
+    const uint32_t t = xs + n;
+    const uint32_t y = fold(t, t + Q, t - Q);
     constexpr uint32_t C = (uint32_t)((1 << (DROP1 - 1)) - Lvl1Int::H + (Lvl1Int::DIGIT_BIAS << DROP1));
     return (uint32_t)((int)(y + C) >> DROP1) ^ (uint32_t)Lvl1Int::DIGIT_BIAS;
   }
-  // ac' + r for r in [-H - 1, H + 1], reduced to [0, Q)
-  __device__ static __forceinline__ uint32_t add(uint32_t acp, int r) {
-    const uint32_t s = acp + (uint32_t)r;
-    return fold(s, s + Q, s - Q);
+  // ac'' + r for r in [0, Q], reduced to [0, Q)
+  __device__ static __forceinline__ uint32_t add(uint32_t acpp, uint32_t r) {
+    const uint32_t s = acpp + r;
+    return min(s, s - Q);
   }
+  template <bool G>
+  __device__ static __forceinline__ uint32_t round(double y, RoundGuard<G> *rg) { return Lvl1Int::round_mod<G>(y, rg); }
 };
 
 // ACC layout: ac[p][h * 8 + e] = coefficient lane + 64 e + 512 h of poly p (0 mask, 1 body).
@@ -96,30 +114,39 @@ __device__ __forceinline__ int acc_coef(int lane, int i) { return lane + 64 * (i
 
 // digits of (X^a - 1) * ACC for both polys. Each poly is staged with its negacyclic extension
 // ext = [ACC, -ACC] (2N int32 = the wave's 8 KB buffer st), so (X^a * ACC)[j] = ext[(j - a) mod 2N]:
-// one masked index and no sign fix-up per coefficient.
-// (ACC in the Lvl1Off representation: ext = [ac', 2H - ac'], every entry "value + H".)
+// no sign fix-up per coefficient. st is 8 KB-aligned (br1f_body), so the LDS byte address of
+// entry (j - a) mod 2N is st | ((4 (lane - a) + 256 i) & 8191) for coefficient j = lane + 64 i:
+// one add and one v_and_or_b32 per read.
+// (ACC in the Lvl1Off representation: ext = [ac'', H - ac''], every entry "value + H/2".)
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
 __device__ __forceinline__ void br1f_digits(const uint32_t (&ac)[2][16], uint32_t *st, int a, int lane,
                                             uint32_t (&pk)[2][16]) {
+  const uint32_t sbase = (uint32_t)(size_t)(lds_u32 *)st;
+  const uint32_t b4 = (uint32_t)(lane - a) * 4u;
+  const uint32_t kWrap = 8u * N1 - 1;  // 8 KB - 1 (no VOP3 literals on gfx9: an SGPR operand)
 #pragma unroll
   for (int p = 0; p < 2; ++p) {
     uint32_t n[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      n[i] = 2 * Lvl1Off::H - ac[p][i];
+      n[i] = Lvl1Off::neg(ac[p][i]);
       st[acc_coef(lane, i)] = ac[p][i];
       st[N1 + acc_coef(lane, i)] = n[i];
     }
     wave_lds_sync();
-    const int base = lane - a + 2 * N1;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) pk[p][i] = Lvl1Off::digits(st[(base + acc_coef(0, i)) & (2 * N1 - 1)], n[i]);
+    for (int i = 0; i < 16; ++i) {  // acc_coef(0, i) = 64 i
+      uint32_t addr;  // ((b4 + 256 i) & 8191) | sbase in one v_and_or_b32 (not formed by the compiler)
+      asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(addr) : "v"(b4 + 256u * i), "s"(kWrap), "v"(sbase));  // one SGPR per VOP3 on gfx9
+      pk[p][i] = Lvl1Off::digits(*(const lds_u32 *)(size_t)addr, n[i]);
+    }
     wave_lds_fence();  // the next poly's writes stay below these reads
   }
 }
 
 // ---- key rows staged through LDS by LDS-DMA ----------------------------------
 // GGSW row q (global row index over the whole key: step * 8 + row) = [A/B][512] complex, 16 KB,
-// copied by the workgroup's waves with global_load_lds_dwordx4 into one of two LDS buffers
+// copied by the workgroup's waves with LDS-DMA (buffer_load_dwordx4 ... lds) into one of two LDS buffers
 // (two barriers per row: one barrier per row exposes the row's load latency, 212 vs 199 ms),
 // transposed so that slot comp * 512 + e * 64 + lane holds the lane's e-th point (the
 // multiply-accumulate then reads consecutive slots: no bank conflicts). Each wave issues
@@ -134,14 +161,24 @@ constexpr int KROW_SLOTS = 2 * Fft512::N;  // double2 per staged row
 __device__ __forceinline__ int key1_pos(int lane, int e) { return e * 64 + lane; }
 constexpr int KROW_INSTR = 16 / BR1F_WPG;  // glds per wave per row
 
-__device__ __forceinline__ void krow_issue(const double2 *__restrict__ row, double2 *buf, int lane,
-                                           int wave) {
+// The key is read through a buffer descriptor (wave-uniform, SGPRs): each DMA instruction is
+// buffer_load_dwordx4 ... offen lds with the lane's byte offset (lane * 16, one VGPR for the whole
+// kernel) and the row / piece offset in soffset, so issuing a row costs no VALU address arithmetic.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t bsk1_rsrc(const double2 *bskf) {
+  constexpr uint32_t bytes = (uint32_t)((size_t)N0 * 2 * D1 * KROW_SLOTS * sizeof(double2));
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<double2 *>(bskf), 0, bytes, 0x00020000);
+}
+__device__ __forceinline__ void krow_issue(__amdgpu_buffer_rsrc_t rsrc, int q,
+                                           double2 *buf, uint32_t lane16, int wave) {
 #pragma unroll
   for (int u = 0; u < KROW_INSTR; ++u) {
     const int ins = wave * KROW_INSTR + u;  // 0..15: comp = ins / 8, point e = ins % 8
     const int comp = ins >> 3, e = ins & 7;
-    const double2 *src = row + comp * Fft512::N + key1_pos(lane, e);
-    __builtin_amdgcn_global_load_lds(src, buf + comp * Fft512::N + e * 64, 16, 0, 0);
+    // key1_pos(lane, e) = e * 64 + lane: the piece starts at slot comp * 512 + e * 64
+    const int piece = comp * Fft512::N + e * 64;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(
+        rsrc, (__attribute__((address_space(3))) void *)(buf + piece), 16, lane16,
+        (int)((uint32_t)q * (uint32_t)(KROW_SLOTS * sizeof(double2)) + (uint32_t)(piece * sizeof(double2))), 0, 0);
   }
 }
 __device__ __forceinline__ void vm_wait_row_in_flight() {  // s_waitcnt vmcnt(KROW_INSTR)
@@ -151,59 +188,75 @@ __device__ __forceinline__ void vm_wait_all() {  // s_waitcnt vmcnt(0)
   __builtin_amdgcn_s_waitcnt((0x7 << 4) | (0xF << 8));
 }
 
+// One GGSW row q = q0 + p D1 + k of a CMUX step: digit k of poly p, forward transform,
+// multiply-accumulate with the staged row. FIRST (the step's row 0) writes the products instead
+// of accumulating, so the accumulators need no zeroing. (A function, not a lambda: a lambda's
+// by-reference captures drop __restrict__, and the pass-0 twiddles were then re-read with vector
+// loads in every row instead of being kept in registers: 3 % slower.)
+template <bool FIRST>
+__device__ __forceinline__ void br1f_row(const uint32_t (&pk)[16], int k, int q, int qtotal, double (&outr)[2][8],
+                                         double (&outi)[2][8], double2 *xch, const double2 *tws,
+                                         __amdgpu_buffer_rsrc_t rsrc, double2 *kbuf, int lane, uint32_t lane16,
+                                         int wave, const double2 *__restrict__ gtw) {
+  using F = Fft512;
+  const bool more = q + 1 < qtotal;
+  wg_barrier_lds();  // every wave has finished reading buffer (q + 1) & 1 (row q - 1)
+  if (more) krow_issue(rsrc, q + 1, kbuf + ((q + 1) & 1) * KROW_SLOTS, lane16, wave);
+  double xr[1][8], xi[1][8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    xr[0][e] = Lvl1Int::digit(pk[e], k);
+    xi[0][e] = Lvl1Int::digit(pk[8 + e], k);
+  }
+  F::fwd<1, true>(xr, xi, xch, tws, lane, gtw);
+  if (more)
+    vm_wait_row_in_flight();  // row q landed (row q + 1 may stay in flight)
+  else
+    vm_wait_all();
+  wg_barrier_lds();  // ... in every wave's share
+  const double2 *kb = kbuf + (q & 1) * KROW_SLOTS;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const double2 ka = kb[e * 64 + lane], kB = kb[F::N + e * 64 + lane];
+    if constexpr (FIRST) {
+      outr[0][e] = __fma_rn(xr[0][e], ka.x, -xi[0][e] * ka.y);
+      outi[0][e] = __fma_rn(xr[0][e], ka.y, xi[0][e] * ka.x);
+      outr[1][e] = __fma_rn(xr[0][e], kB.x, -xi[0][e] * kB.y);
+      outi[1][e] = __fma_rn(xr[0][e], kB.y, xi[0][e] * kB.x);
+    } else {
+      outr[0][e] = __fma_rn(xr[0][e], ka.x, __fma_rn(-xi[0][e], ka.y, outr[0][e]));
+      outi[0][e] = __fma_rn(xr[0][e], ka.y, __fma_rn(xi[0][e], ka.x, outi[0][e]));
+      outr[1][e] = __fma_rn(xr[0][e], kB.x, __fma_rn(-xi[0][e], kB.y, outr[1][e]));
+      outi[1][e] = __fma_rn(xr[0][e], kB.y, __fma_rn(xi[0][e], kB.x, outi[1][e]));
+    }
+  }
+}
+
 // One CMUX step with LDS-staged key rows. q0 = first global row of this step; rows q0..q0+7 are
 // consumed, the next step's first row is prefetched on the way. xch: the wave's exchange buffer
 // (Fft512::BUF).
 template <bool G>
 __device__ __forceinline__ void br1f_step_lds(uint32_t (&ac)[2][16], double2 *xch, const double2 *tws, int a,
-                                              const double2 *__restrict__ bskf, int q0, int qtotal,
-                                              double2 *kbuf, int lane, int wave,
+                                              __amdgpu_buffer_rsrc_t rsrc, int q0, int qtotal, double2 *kbuf,
+                                              int lane, uint32_t lane16, int wave,
                                               const double2 *__restrict__ gtw, RoundGuard<G> &rg) {
   using F = Fft512;
   uint32_t pk[2][16];
   br1f_digits(ac, reinterpret_cast<uint32_t *>(xch), a, lane, pk);
   double outr[2][8], outi[2][8];
-#pragma unroll
-  for (int o = 0; o < 2; ++o)
-#pragma unroll
-    for (int e = 0; e < 8; ++e) outr[o][e] = outi[o][e] = 0.0;
-#pragma unroll
-  for (int p = 0; p < 2; ++p) {
+  br1f_row<true>(pk[0], 0, q0, qtotal, outr, outi, xch, tws, rsrc, kbuf, lane, lane16, wave, gtw);
 #pragma unroll 1
-    for (int k = 0; k < D1; ++k) {
-      const int q = q0 + p * D1 + k;
-      const bool more = q + 1 < qtotal;
-      wg_barrier_lds();  // every wave has finished reading buffer (q + 1) & 1 (row q - 1)
-      if (more) krow_issue(bskf + (size_t)(q + 1) * KROW_SLOTS, kbuf + ((q + 1) & 1) * KROW_SLOTS, lane, wave);
-      double xr[1][8], xi[1][8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        xr[0][e] = Lvl1Int::digit(pk[p][e], k);
-        xi[0][e] = Lvl1Int::digit(pk[p][8 + e], k);
-      }
-      F::fwd<1, true>(xr, xi, xch, tws, lane, gtw);
-      if (more)
-        vm_wait_row_in_flight();  // row q landed (row q + 1 may stay in flight)
-      else
-        vm_wait_all();
-      wg_barrier_lds();  // ... in every wave's share
-      const double2 *kb = kbuf + (q & 1) * KROW_SLOTS;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const double2 ka = kb[e * 64 + lane], kB = kb[F::N + e * 64 + lane];
-        outr[0][e] = __fma_rn(xr[0][e], ka.x, __fma_rn(-xi[0][e], ka.y, outr[0][e]));
-        outi[0][e] = __fma_rn(xr[0][e], ka.y, __fma_rn(xi[0][e], ka.x, outi[0][e]));
-        outr[1][e] = __fma_rn(xr[0][e], kB.x, __fma_rn(-xi[0][e], kB.y, outr[1][e]));
-        outi[1][e] = __fma_rn(xr[0][e], kB.y, __fma_rn(xi[0][e], kB.x, outi[1][e]));
-      }
-    }
-  }
+  for (int k = 1; k < D1; ++k)
+    br1f_row<false>(pk[0], k, q0 + k, qtotal, outr, outi, xch, tws, rsrc, kbuf, lane, lane16, wave, gtw);
+#pragma unroll 1
+  for (int k = 0; k < D1; ++k)
+    br1f_row<false>(pk[1], k, q0 + D1 + k, qtotal, outr, outi, xch, tws, rsrc, kbuf, lane, lane16, wave, gtw);
   F::inv_pair<true>(outr, outi, xch, tws, lane, gtw);  // both outputs, interleaved
 #pragma unroll
   for (int o = 0; o < 2; ++o)
 #pragma unroll
     for (int i = 0; i < 16; ++i)
-      ac[o][i] = Lvl1Off::add(ac[o][i], Lvl1Int::round_red<G>(i < 8 ? outr[o][i] : outi[o][i - 8], &rg));
+      ac[o][i] = Lvl1Off::add(ac[o][i], Lvl1Off::round<G>(i < 8 ? outr[o][i] : outi[o][i - 8], &rg));
 }
 
 // Level-1 blind rotations: BR1F_WPG waves per workgroup, one rotation per wave; rotation
@@ -219,11 +272,14 @@ __device__ __forceinline__ void br1f_body(
     uint64_t *__restrict__ rlwe_out, int mode, size_t nrot, unsigned long long *margin) {
   constexpr int NF = Fft512::N, W = BR1F_WPG;
   static_assert(16 % W == 0, "LDS key staging: W divides the row's 16 one-KiB pieces");
-  __shared__ double2 xch_all[W][Fft512::BUF];
+  __shared__ __attribute__((aligned(8192))) double2 xch_all[W][Fft512::BUF];  // br1f_digits' addressing
+  static_assert(Fft512::BUF * sizeof(double2) == 8192, "one 8 KB buffer per wave");
   __shared__ double2 tws[NF];
   __shared__ uint16_t la_all[W][N0];
   __shared__ double2 kbuf[2 * KROW_SLOTS];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // the wave index is wave-uniform: readfirstlane keeps it (and every key-row DMA address and M0
+  // value derived from it) in SGPRs instead of per-lane VALU arithmetic
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   double2 *xch = xch_all[wave];
   uint16_t *la = la_all[wave];
   const size_t g = (size_t)blockIdx.x * W + wave;
@@ -241,23 +297,25 @@ __device__ __forceinline__ void br1f_body(
     b = lwe_b[gi] & (Q0 - 1);
   }
   // ACC = (0, X^{-b} * LUT1)
-  uint32_t ac[2][16];  // Lvl1Off: ac + H
+  uint32_t ac[2][16];  // Lvl1Off: ac + OFF
   const int r0 = (2 * N1 - (b % (2 * N1))) % (2 * N1);
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
-    ac[0][i] = Lvl1Off::H;
-    ac[1][i] = (uint32_t)((int)canon_small<Mod<1>>(rot_read<N1>(tb.lut1, acc_coef(lane, i), r0)) + Lvl1Int::H);
+    ac[0][i] = Lvl1Off::enc(0);
+    ac[1][i] = Lvl1Off::enc((int)canon_small<Mod<1>>(rot_read<N1>(tb.lut1, acc_coef(lane, i), r0)));
   }
   for (int j = threadIdx.x; j < NF; j += 64 * W) tws[j] = tb.fft1[j];
   __syncthreads();
   // every step runs (a = 0 gives zero digits and leaves ACC unchanged) so the waves share the
   // staged key rows; row 0 is issued before the loop
-  krow_issue(bskf, kbuf, lane, wave);
+  const __amdgpu_buffer_rsrc_t rsrc = bsk1_rsrc(bskf);
+  const uint32_t lane16 = (uint32_t)lane * 16u;
+  krow_issue(rsrc, 0, kbuf, lane16, wave);
   RoundGuard<G> rg;
 #pragma unroll 1
   for (int i = 0; i < N0; ++i) {
     const int a = __builtin_amdgcn_readfirstlane(la[i]);
-    br1f_step_lds<G>(ac, xch, tws, a, bskf, i * 2 * D1, N0 * 2 * D1, kbuf, lane, wave, tb.fft1, rg);
+    br1f_step_lds<G>(ac, xch, tws, a, rsrc, i * 2 * D1, N0 * 2 * D1, kbuf, lane, lane16, wave, tb.fft1, rg);
   }
   rg.publish(margin);
   __syncthreads();
@@ -265,7 +323,7 @@ __device__ __forceinline__ void br1f_body(
   if (mode == 0) {  // extract_lwe_locally (coefficient 0), detector.rs:561
     int *st = reinterpret_cast<int *>(xch);
 #pragma unroll
-    for (int i = 0; i < 16; ++i) st[acc_coef(lane, i)] = (int)ac[0][i] - Lvl1Int::H;
+    for (int i = 0; i < 16; ++i) st[acc_coef(lane, i)] = Lvl1Off::dec(ac[0][i]);
     wave_lds_sync();
     uint32_t *o = ext + g * (N1 + 1);
 #pragma unroll
@@ -273,13 +331,13 @@ __device__ __forceinline__ void br1f_body(
       const int j = acc_coef(lane, i);
       o[j] = Lvl1Int::to_u32(j == 0 ? st[0] : -st[N1 - j]);
     }
-    if (lane == 0) o[N1] = Lvl1Int::to_u32((int)ac[1][0] - Lvl1Int::H);
+    if (lane == 0) o[N1] = Lvl1Int::to_u32(Lvl1Off::dec(ac[1][0]));
   } else {
     uint64_t *o = rlwe_out + g * 2 * N1;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      o[acc_coef(lane, i)] = Lvl1Int::to_u32((int)ac[0][i] - Lvl1Int::H);
-      o[N1 + acc_coef(lane, i)] = Lvl1Int::to_u32((int)ac[1][i] - Lvl1Int::H);
+      o[acc_coef(lane, i)] = Lvl1Int::to_u32(Lvl1Off::dec(ac[0][i]));
+      o[N1 + acc_coef(lane, i)] = Lvl1Int::to_u32(Lvl1Off::dec(ac[1][i]));
     }
   }
 }

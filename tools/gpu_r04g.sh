@@ -1,0 +1,9 @@
+# br1f instruction-diet ablation: base (HEAD), all changes, without the buffer DMA, without the
+# peeled first row, representation only (+ SGPR wave), representation only (VGPR wave); twice.
+set -o pipefail
+out=gpurun_out/r04g
+mkdir -p $out
+rm -f gpurun_out/bench_variants.log
+tools/bench_variants.sh 16384 --no-e2e || exit 2
+tools/bench_variants.sh 16384 --no-e2e || exit 3
+cp gpurun_out/bench_variants.log $out/ab.log

@@ -1,0 +1,8 @@
+# br1f ablation 3 (restrict-preserving row function): base, buffer DMA + peel, without peel, without buffer DMA, + floor rounding and H/2 offset, + v_and_or addresses; twice.
+set -o pipefail
+out=gpurun_out/r04i
+mkdir -p $out
+rm -f gpurun_out/bench_variants.log
+tools/bench_variants.sh 16384 --no-e2e || exit 2
+tools/bench_variants.sh 16384 --no-e2e || exit 3
+cp gpurun_out/bench_variants.log $out/ab.log
