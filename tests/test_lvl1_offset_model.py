@@ -1,4 +1,4 @@
-"""Integer model of br1f's accumulator representation (tfhe-omr_amd/csrc/br1_fft.hpp, Lvl1Off and
+"""Integer models of br1f's accumulator representation (tfhe-omr_amd/csrc/br1_fft.hpp, Lvl1Off and
 Lvl1Int::round_mod), in numpy with explicit u32 wrap-around, against the plain definitions:
 
 - ac'' = ac + H/2 (mod Q) in [0, Q); the stored negacyclic half n = H - ac'' (signed u32);
@@ -6,7 +6,9 @@ Lvl1Int::round_mod), in numpy with explicit u32 wrap-around, against the plain d
   Lvl1Int::digits(canon(x - ac)), i.e. the NonPowOf2ApproxSignedBasis digits (logB 5, d 4, drop 7)
   of the reference's decomposition (detector.rs:553-557 via the level-1 parameters);
 - round_mod(y) in [0, Q] with round_mod(y) = round(y) mod Q, and add(ac'', r) = ac'' + r (mod Q)
-  in [0, Q), for FFT outputs y = integer + e (|y| < 2^43, |e| < 0.1), including the multiples of q.
+  in [0, Q), for FFT outputs y = integer + e (|y| < 2^43, |e| < 0.1), including the multiples of q;
+- and br2f's level-2 digit words (Digits2S: two's-complement fields, one v_bfe_i32 per digit) give
+  the same six digits as Digits2 (detect_kernels.hpp) over the whole canonical range of q2.
 """
 import numpy as np
 
@@ -117,3 +119,45 @@ def test_round_mod_and_update():
     got = add(a, r)
     assert np.all((got >= 0) & (got < Q))
     assert np.array_equal(dec(got), canon(dec(a) + ints))
+
+
+# ---- level 2: br2f's signed-field digit words (Digits2S, tfhe-omr_amd/csrc/br2_fft.hpp) --------
+def _digits2_ref(v):
+    """Digits2 (detect_kernels.hpp): biased 7-bit fields (the top one 8 bits wide), minus 64."""
+    y = np.floor(v / 256.0 + 0.5) + 2216338399296.0  # v / 256 is exact: the kernel's fma
+    hi = np.floor(y * (1.0 / 2097152.0))
+    lo = y - hi * 2097152.0
+    w = [lo.astype(np.int64), hi.astype(np.int64)]
+    out = []
+    for k in range(6):
+        h, j = divmod(k, 3)
+        width = 8 if j == 2 else 7
+        out.append(((w[h] >> (7 * j)) & ((1 << width) - 1)) - 64)
+    return np.stack(out)
+
+
+def _digits2s(v):
+    y = np.floor(v / 256.0 + 0.5) + 17315143744.0
+    hi = np.floor(y * (1.0 / 2097152.0))
+    lo = y - hi * 2097152.0
+    w0 = u32(lo.astype(np.int64)) ^ 0x102040
+    w1 = u32(hi.astype(np.int64)) ^ 0x2040
+    out = []
+    for k in range(6):
+        h, j = divmod(k, 3)
+        w = s32(w0 if h == 0 else w1)
+        width = 18 if (h == 1 and j == 2) else 7
+        f = (w >> (7 * j)) & ((1 << width) - 1)
+        out.append(np.where(f >= 1 << (width - 1), f - (1 << width), f))
+    return np.stack(out)
+
+
+def test_level2_signed_digit_fields_match_digits2():
+    Q2 = 1125899906826241  # SecondLevelField, see tfhe-omr_amd/csrc/common.hpp OMR_Q2
+    h2 = Q2 // 2
+    rng = np.random.default_rng(4)
+    v = np.concatenate([rng.integers(-h2, h2 + 1, 300000), np.array([-h2, h2, 0, 1, -1, 127, 128, -128, -129]),
+                        np.arange(-2000, 2000) * 256 + 128]).astype(np.float64)
+    assert np.array_equal(_digits2s(v), _digits2_ref(v))
+    d = _digits2s(v)
+    assert np.array_equal(sum(d[k] * 128 ** k for k in range(6)), np.floor(v / 256.0 + 0.5).astype(np.int64))
