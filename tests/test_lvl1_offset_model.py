@@ -2,8 +2,8 @@
 Lvl1Int::round_mod), in numpy with explicit u32 wrap-around, against the plain definitions:
 
 - ac'' = ac + H/2 (mod Q) in [0, Q); the stored negacyclic half n = H - ac'' (signed u32);
-- the digit word from a rotated entry x'' (either half) and the lane's own n equals
-  Lvl1Int::digits(canon(x - ac)), i.e. the NonPowOf2ApproxSignedBasis digits (logB 5, d 4, drop 7)
+- the digits of the word from a rotated entry x'' (either half) and the lane's own n equal
+  those of Lvl1Int::digits(canon(x - ac)), i.e. the NonPowOf2ApproxSignedBasis digits (logB 5, d 4, drop 7)
   of the reference's decomposition (detector.rs:553-557 via the level-1 parameters);
 - round_mod(y) in [0, Q] with round_mod(y) = round(y) mod Q, and add(ac'', r) = ac'' + r (mod Q)
   in [0, Q), for FFT outputs y = integer + e (|y| < 2^43, |e| < 0.1), including the multiples of q;
@@ -59,11 +59,26 @@ def neg(a):
     return u32(H - a)
 
 
-def off_digits(xs, n):
+def off_digits(xs, n):  # Lvl1Off::digits_u: the word shifted left by DROP (low bits: remainder)
     t = u32(xs + n)
     y = np.minimum(np.minimum(t, u32(t + Q)), u32(t - Q))
     C = (1 << (DROP - 1)) - H + (BIAS << DROP)
-    return u32((s32(y + C) >> DROP) ^ BIAS)
+    return u32(u32(y + C) ^ (BIAS << DROP))
+
+
+def off_digit(w, k):  # a signed bit-field extract at offset DROP + 5k
+    w = u32(w)
+    if k < D - 1:
+        f = (w >> (DROP + LOGB * k)) & 31
+        return np.where(f >= 16, f - 32, f)
+    return s32(w) >> (DROP + LOGB * (D - 1))
+
+
+def off_digit_shifts(w, k):  # Lvl1Off::digit_shifts_u
+    w = u32(w)
+    s1 = 32 - DROP - LOGB * (k + 1) if k < D - 1 else 0
+    s2 = 32 - LOGB if k < D - 1 else DROP + LOGB * (D - 1)
+    return s32(u32(w << s1)) >> s2
 
 
 def round_mod(y):
@@ -96,7 +111,10 @@ def test_digit_words_match_the_decomposition():
     for xs in (enc(x), neg(enc(-x))):  # x read from the first half, or -x's entry in the second
         got = off_digits(xs, n)
         want = ref_digits(canon(x - ac))
-        assert np.array_equal(got, want)
+        assert np.array_equal(u32(s32(got) >> DROP), want)  # Lvl1Off::digits (br1f)
+        for k in range(D):  # Lvl1Off::digits_u + digit_shifts_u (br1l)
+            assert np.array_equal(off_digit_shifts(got, k), digit(want, k))
+            assert np.array_equal(off_digit(got, k), digit(want, k))
     # and the digits recompose the rounded value (the basis of detector.rs's decomposition)
     w = ref_digits(canon(x - ac))
     val = sum(digit(w, k) * (32 ** k) for k in range(D))

@@ -76,8 +76,8 @@ struct Lvl1Int {
 // t = x'' + n = (x - ac) + H (mod Q) with t in (-Q, 2Q), so one v_min3_u32(t, t + Q, t - Q) (the
 // wrapped operands lose) is canon(x - ac) + H in [0, Q), and the digit word of the canonical
 // residue y - H is ((y - H + 2^6 + 2^7 DIGIT_BIAS) >> 7) ^ DIGIT_BIAS (the bias folded in before
-// the shift): 6 integer operations per digit word. The accumulator update adds a rounded product
-// in [0, Q] (Lvl1Int::round_mod): s in [0, 2Q), min(s, s - Q), 3 operations.
+// the shift): 6 integer operations per word (5 in br1l, digits_u). The accumulator update adds a
+// rounded product in [0, Q] (Lvl1Int::round_mod): s in [0, 2Q), min(s, s - Q), 3 operations.
 struct Lvl1Off {
   static constexpr uint32_t Q = (uint32_t)Lvl1Int::Q, H = (uint32_t)Lvl1Int::H, OFF = H / 2;
   static_assert(H % 2 == 0, "H/2 offset");
@@ -93,12 +93,26 @@ struct Lvl1Off {
   __device__ static __forceinline__ int dec(uint32_t acpp) { return Lvl1Int::canon((int)acpp - (int)OFF); }
   // the stored negacyclic half "-ac + H/2" and the digit operand
   __device__ static __forceinline__ uint32_t neg(uint32_t acpp) { return H - acpp; }
-  // digit word of canon(x - ac) from a stored entry x'' and n = neg(ac''): t = x - ac + H
+  // digit word of canon(x - ac) from a stored entry x'' and n = neg(ac''): t = x - ac + H; the
+  // Lvl1Int::digits word (extract with Lvl1Int::digit / digit_shifts)
   __device__ static __forceinline__ uint32_t digits(uint32_t xs, uint32_t n) {
+    return (uint32_t)((int)digits_u(xs, n) >> DROP1);  // arithmetic: the top digit is signed
+  }
+  // the same word before the shift by DROP1 (bits 7.. hold the fields, bits 0..6 the dropped
+  // remainder, never read): the shift folds into the extraction offsets (digit_shifts_u), one
+  // operation fewer per word. br1l uses it; in br1f the unshifted words changed the register
+  // allocation (9 spills), so br1f keeps the shifted word.
+  __device__ static __forceinline__ uint32_t digits_u(uint32_t xs, uint32_t n) {
     const uint32_t t = xs + n;
     const uint32_t y = fold(t, t + Q, t - Q);
     constexpr uint32_t C = (uint32_t)((1 << (DROP1 - 1)) - Lvl1Int::H + (Lvl1Int::DIGIT_BIAS << DROP1));
-    return (uint32_t)((int)(y + C) >> DROP1) ^ (uint32_t)Lvl1Int::DIGIT_BIAS;
+    return (y + C) ^ ((uint32_t)Lvl1Int::DIGIT_BIAS << DROP1);
+  }
+  // signed digit k of a digits_u() word by two shifts
+  __device__ static __forceinline__ double digit_shifts_u(uint32_t w, int k) {
+    const int s1 = k < D1 - 1 ? 32 - DROP1 - LOGB1 * (k + 1) : 0;
+    const int s2 = k < D1 - 1 ? 32 - LOGB1 : DROP1 + LOGB1 * (D1 - 1);
+    return (double)((int)(w << s1) >> s2);
   }
   // ac'' + r for r in [0, Q], reduced to [0, Q)
   __device__ static __forceinline__ uint32_t add(uint32_t acpp, uint32_t r) {

@@ -258,6 +258,86 @@ __device__ __forceinline__ int key_pos(int t, int e) { return e * Fft1024::T + t
 // [670][12][2 out][2 limb][1024], point idx(4, t, e) at key_pos(t, e): key_spectrum_dd_kernel<2>
 // (key_spectra.hpp), in double-double.
 
+// Level-2 digit words for br2f: the Digits2 decomposition (NonPowOf2ApproxSignedBasis logB 7,
+// d 6, drop 8) with every field a two's-complement digit, so that each digit is one v_bfe_i32
+// (Digits2's biased fields need a v_bfe_u32 and a subtraction of 64). Digits 0..4 are biased by 64
+// as in Digits2 (so the words have no borrows) and each 7-bit field is then XORed with 64
+// ((f - 64) mod 128 = f ^ 64); the top digit d5 is left unbiased, so hi = floor(y / 2^21) holds it
+// as a signed value in bits 14..31 (sign-extended by the extract).
+struct Digits2S {
+  static constexpr int DW = 2;
+  static_assert(LOGB2 == 7 && D2 == 6 && DROP2 == 8, "closed form written for the level-2 basis");
+  __device__ static __forceinline__ void pack(double v, uint32_t (&pk)[DW]) {
+    const double y = floor(__fma_rn(v, 1.0 / 256.0, 0.5)) + 17315143744.0;  // + 64 (1 + 128 + .. + 128^4)
+    const double hi = floor(y * (1.0 / 2097152.0));
+    const double lo = __fma_rn(-hi, 2097152.0, y);
+    pk[0] = (uint32_t)(int)lo ^ 0x102040u;   // fields 0, 1, 2
+    pk[1] = (uint32_t)(int)hi ^ 0x2040u;     // fields 3, 4; d5 in bits 14..
+  }
+  // digit j + 3 h as a double (h: the word, a compile-time constant)
+  template <int H>
+  __device__ static __forceinline__ double digit(const uint32_t (&pk)[DW], int j) {
+    return (double)(int)__builtin_amdgcn_sbfe(pk[H], 7 * j, H == 1 && j == 2 ? 18 : 7);
+  }
+};
+
+// BSK2 (FFT form) through a buffer descriptor: each key load is buffer_load_dwordx4 with the
+// thread's byte offset (t * 16) in voffset and the row / block / register offset in soffset, so a
+// digit's 16 loads cost no VALU address arithmetic (64-bit VGPR address adds before).
+constexpr int BR2_ROW = 4 * Fft1024::n;  // double2 per GGSW row: [2 out][2 limb][1024]
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t bsk2_rsrc(const double2 *bskf) {
+  constexpr uint32_t bytes = (uint32_t)((size_t)NI * 2 * D2 * BR2_ROW * sizeof(double2));
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<double2 *>(bskf), 0, bytes, 0x00020000);
+}
+typedef unsigned br2_v4u __attribute__((ext_vector_type(4)));
+// output o's two limb blocks of global row q: thread t's 4 points (key_pos(t, e) = e * 256 + t)
+__device__ __forceinline__ void br2f_load_half(double2 (&k)[2][Fft1024::E], __amdgpu_buffer_rsrc_t rsrc, int q,
+                                               int o, uint32_t t16) {
+#pragma unroll
+  for (int l = 0; l < 2; ++l)
+#pragma unroll
+    for (int e = 0; e < Fft1024::E; ++e) {
+      const uint32_t soff = (uint32_t)q * (uint32_t)(BR2_ROW * sizeof(double2)) +
+                            (uint32_t)(((o * 2 + l) * Fft1024::n + e * Fft1024::T) * sizeof(double2));
+      k[l][e] = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rsrc, t16, (int)soff, 0));
+    }
+}
+
+// One digit of a CMUX step: forward transform of digit j + 3 w of poly p (its words pk), then the
+// multiply-accumulate into the four (output, limb) spectra: output A with ka (loaded one digit
+// ahead), output B with kb (loaded after the transform); ka is reloaded for the next digit nx
+// between the two.
+// (A function, not a lambda: by-reference captures drop __restrict__ / address-space facts.)
+template <int W>
+__device__ __forceinline__ void br2f_digit(const uint32_t (&pk)[2][Fft1024::E][Digits2S::DW], int j, int q, int nx,
+                                           double (&sr)[2][2][Fft1024::E], double (&si)[2][2][Fft1024::E],
+                                           double2 (&ka)[2][Fft1024::E], double2 (&kb)[2][Fft1024::E],
+                                           double2 *X, double2 *Wb, const double2 *tws, __amdgpu_buffer_rsrc_t rsrc,
+                                           uint32_t t16, int t) {
+  using F = Fft1024;
+  constexpr int E = F::E;
+  double xr[E], xi[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    xr[e] = Digits2S::digit<W>(pk[0][e], j);
+    xi[e] = Digits2S::digit<W>(pk[1][e], j);
+  }
+  F::fwd(xr, xi, X, Wb, tws, t);
+  br2f_load_half(kb, rsrc, q, 1, t16);
+#pragma unroll
+  for (int o = 0; o < 2; ++o) {
+#pragma unroll
+    for (int l = 0; l < 2; ++l)
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const double2 kv = o ? kb[l][e] : ka[l][e];
+        sr[o][l][e] = __fma_rn(xr[e], kv.x, __fma_rn(-xi[e], kv.y, sr[o][l][e]));
+        si[o][l][e] = __fma_rn(xr[e], kv.y, __fma_rn(xi[e], kv.x, si[o][l][e]));
+      }
+    if (o == 0) br2f_load_half(ka, rsrc, nx, 0, t16);
+  }
+}
+
 // Level-2 blind rotation (BlindRotationKey::blind_rotate, detector.rs:623) on the exact FFT: one
 // 256-thread workgroup per message, ACC in registers (P0 layout: coefficients j and j + 1024 of the
 // thread's 4 points), output the coefficient-domain rotation u64 [2][2048] (trace_kernel follows).
@@ -276,7 +356,6 @@ __device__ __forceinline__ void br2f_body(const uint32_t *__restrict__ lwe_int, 
                                           unsigned long long *margin) {
   using F = Fft1024;
   using M = Mod<2>;
-  using DG = Digits2;
   constexpr int E = F::E, NN = N2;
   static_assert(F::TW_LEN <= F::n, "the twiddle table's LDS doubles as the trace's NTT table");
   __shared__ double2 tws[F::n];
@@ -306,30 +385,19 @@ __device__ __forceinline__ void br2f_body(const uint32_t *__restrict__ lwe_int, 
   // multiply-accumulate): 32 VGPRs fewer across the transform. Loading them earlier (before or
   // inside the transform) measured 43-50 % slower (profiles/r03/level2_experiments.log).
   double2 ka[2][E], kb[2][E];
-  auto load_half = [&](double2 (&k)[2][E], const double2 *row, int o) {
-#pragma unroll
-    for (int l = 0; l < 2; ++l)
-#pragma unroll
-      for (int e = 0; e < E; ++e) k[l][e] = row[(o * 2 + l) * F::n + key_pos(t, e)];
-  };
-  constexpr size_t ROW = 4 * F::n;  // double2 per GGSW row
+  const __amdgpu_buffer_rsrc_t rsrc = bsk2_rsrc(bskf);
+  const uint32_t t16 = (uint32_t)t * 16u;
   RoundGuard<G> rg;
 #pragma unroll 1
   for (int i = 0; i < NI; ++i) {
     const int a = (int)__builtin_amdgcn_readfirstlane(lwe[i]) & (2 * NN - 1);
     if (a == 0) continue;  // (X^0 - 1) * ACC = 0
-    const double2 *step = bskf + (size_t)i * 2 * D2 * ROW;
-    load_half(ka, step, 0);
+    const int q0 = i * 2 * D2;  // the step's first global row
+    br2f_load_half(ka, rsrc, q0, 0, t16);
     double sr[2][2][E], si[2][2][E];  // [output][limb] spectra
 #pragma unroll
-    for (int o = 0; o < 2; ++o)
-#pragma unroll
-      for (int l = 0; l < 2; ++l)
-#pragma unroll
-        for (int e = 0; e < E; ++e) sr[o][l][e] = si[o][l][e] = 0.0;
-#pragma unroll
     for (int p = 0; p < 2; ++p) {
-      uint32_t pk[2][E][DG::DW];  // [coefficient j / j + 1024][point] digit words
+      uint32_t pk[2][E][Digits2S::DW];  // [coefficient j / j + 1024][point] digit words
       {  // digits of (X^a - 1) * ACC_p, staged in X1 (mask) / X0 (body)
         double *st = reinterpret_cast<double *>(Xb[p == 0 ? 1 : 0]);
 #pragma unroll
@@ -346,7 +414,7 @@ __device__ __forceinline__ void br2f_body(const uint32_t *__restrict__ lwe_int, 
             const uint32_t vh = (uint32_t)(__builtin_bit_cast(uint64_t, v) >> 32) ^ ((u & NN) << (31 - 11));
             const double rot = __builtin_bit_cast(double, (__builtin_bit_cast(uint64_t, v) & 0xffffffffull) |
                                                               ((uint64_t)vh << 32));
-            DG::pack(canon_small<M>(rot - ac[p][h][e]), pk[h][e]);
+            Digits2S::pack(canon_small<M>(rot - ac[p][h][e]), pk[h][e]);
             // keep the words as integers (not the doubles they come from) across the digit loop
             asm volatile("" : "+v"(pk[h][e][0]), "+v"(pk[h][e][1]));
           }
@@ -355,36 +423,25 @@ __device__ __forceinline__ void br2f_body(const uint32_t *__restrict__ lwe_int, 
       }
       // digits in issue order g = 2 j + w: digit j + 3 w sits in word w at field j, so the word is
       // chosen at compile time; its GGSW row is p D2 + j + 3 w. Cross-wave buffers: mask digits X0,
-      // X1, ..., body digits X1, X0, ... (X_{(w + p) & 1}).
+      // X1, ..., body digits X1, X0, ... (X_{(w + p) & 1}). The next digit in issue order (the last
+      // digit reloads its own row: harmless): after (j, 0) comes (j, 1), after (j, 1) (j + 1, 0),
+      // after the mask's last digit the body's first, after the body's last itself.
+      auto nxt = [&](int j, int w) {
+        return q0 + (w == 0 ? p * D2 + j + 3 : (j + 1 < D2 / 2 ? p * D2 + j + 1 : (p == 0 ? D2 : 2 * D2 - 1)));
+      };
+      if (p == 0) {  // (peeling the step's first digit instead measured 10 % slower: 22 spills)
+#pragma unroll
+        for (int o = 0; o < 2; ++o)
+#pragma unroll
+          for (int l = 0; l < 2; ++l)
+#pragma unroll
+            for (int e = 0; e < E; ++e) sr[o][l][e] = si[o][l][e] = 0.0;
+      }
 #pragma unroll 1
       for (int j = 0; j < D2 / 2; ++j) {
-#pragma unroll
-        for (int w = 0; w < 2; ++w) {
-          double xr[E], xi[E];
-#pragma unroll
-          for (int e = 0; e < E; ++e) {
-            xr[e] = (double)((int)__builtin_amdgcn_ubfe(pk[0][e][w], 7 * j, j == 2 ? 8 : 7) - 64);
-            xi[e] = (double)((int)__builtin_amdgcn_ubfe(pk[1][e][w], 7 * j, j == 2 ? 8 : 7) - 64);
-          }
-          const double2 *row = step + (size_t)(p * D2 + j + 3 * w) * ROW;
-          // the next digit's row in issue order (the last digit reloads its own: harmless)
-          const int nx = w == 0 ? p * D2 + j + 3 : (j + 1 < D2 / 2 ? p * D2 + j + 1 : (p == 0 ? D2 : 2 * D2 - 1));
-          const double2 *next = step + (size_t)nx * ROW;
-          F::fwd(xr, xi, Xb[(w + p) & 1], W, tws, t);
-          load_half(kb, row, 1);
-#pragma unroll
-          for (int o = 0; o < 2; ++o) {
-#pragma unroll
-            for (int l = 0; l < 2; ++l)
-#pragma unroll
-              for (int e = 0; e < E; ++e) {
-                const double2 kv = o ? kb[l][e] : ka[l][e];
-                sr[o][l][e] = __fma_rn(xr[e], kv.x, __fma_rn(-xi[e], kv.y, sr[o][l][e]));
-                si[o][l][e] = __fma_rn(xr[e], kv.y, __fma_rn(xi[e], kv.x, si[o][l][e]));
-              }
-            if (o == 0) load_half(ka, next, 0);
-          }
-        }
+        br2f_digit<0>(pk, j, q0 + p * D2 + j, nxt(j, 0), sr, si, ka, kb, Xb[p & 1], W, tws, rsrc, t16, t);
+        br2f_digit<1>(pk, j, q0 + p * D2 + j + 3, nxt(j, 1), sr, si, ka, kb, Xb[(1 + p) & 1], W, tws, rsrc, t16,
+                      t);
       }
     }
     // inverses (X1, X0, X1, X0), rounding to the exact limb products, recombination mod q2

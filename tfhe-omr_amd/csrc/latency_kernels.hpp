@@ -82,7 +82,8 @@ __device__ __forceinline__ void br1l_body(
   using F = Fft512;
   constexpr int NF = F::N, W = BR1L_WAVES;
   static_assert(W == 8 && NF == 8 * 64, "one wave per GGSW row and per register slot");
-  __shared__ int ext[2][2 * N1];              // [ACC, -ACC] per poly (0 mask, 1 body)
+  // [ACC, -ACC] per poly (0 mask, 1 body), Lvl1Off form; 8 KB-aligned for the v_and_or addresses
+  __shared__ __attribute__((aligned(8192))) uint32_t ext[2][2 * N1];
   __shared__ double2 xch_all[W][F::BUF];      // per wave: its transform's exchange, then its spectrum [e][lane]
   __shared__ double2 outs[2][8 * 64];         // outputs A, B: [e][lane]
   __shared__ double2 tws[NF];
@@ -105,15 +106,17 @@ __device__ __forceinline__ void br1l_body(
   }
   const int r0 = (2 * N1 - (b % (2 * N1))) % (2 * N1);
   // ACC = (0, X^{-b} * LUT1): wave 0 owns the mask accumulator, wave 1 the body accumulator
-  int ac[16];
+  // (the accumulator in br1f's Lvl1Off form: ac'' = ac + H/2 in [0, Q), the stored negacyclic half
+  // H - ac'' doubling as the digit operand; br1_fft.hpp, tests/test_lvl1_offset_model.py)
+  uint32_t ac[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i)
-    ac[i] = wave == 1 ? (int)canon_small<Mod<1>>(rot_read<N1>(tb.lut1, acc_coef(lane, i), r0)) : 0;
+    ac[i] = Lvl1Off::enc(wave == 1 ? (int)canon_small<Mod<1>>(rot_read<N1>(tb.lut1, acc_coef(lane, i), r0)) : 0);
   if (wave < 2) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       ext[wave][acc_coef(lane, i)] = ac[i];
-      ext[wave][N1 + acc_coef(lane, i)] = -ac[i];
+      ext[wave][N1 + acc_coef(lane, i)] = Lvl1Off::neg(ac[i]);
     }
   }
   for (int j = threadIdx.x; j < NF; j += 64 * W) tws[j] = tb.fft1[j];
@@ -144,19 +147,23 @@ __device__ __forceinline__ void br1l_body(
     const int a = __builtin_amdgcn_readfirstlane(la[i]);  // != 0: (X^0 - 1) * ACC = 0 is skipped
     OMR_PHASE(pslot, hs, 0);
     double xr[1][8], xi[1][8];
-    const int base = lane - a + 2 * N1;
+    const uint32_t sbase = (uint32_t)(size_t)(lds_u32 *)ext[p], b4 = (uint32_t)(lane - a) * 4u;
+    const uint32_t kWrap = 8u * N1 - 1;  // as br1f_digits: ((b4 + 256 q) & 8191) | sbase
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int j = acc_coef(lane, q);
-      const uint32_t w = Lvl1Int::digits(Lvl1Int::canon(ext[p][(base + acc_coef(0, q)) & (2 * N1 - 1)] - ext[p][j]));
-      const double d = Lvl1Int::digit_shifts(w, k);
+      uint32_t addr;
+      asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(addr) : "v"(b4 + 256u * q), "s"(kWrap), "v"(sbase));
+      const uint32_t w = Lvl1Off::digits_u(*(const lds_u32 *)(size_t)addr, ext[p][N1 + j]);
+      const double d = Lvl1Off::digit_shifts_u(w, k);
       if (q < 8)
         xr[0][q] = d;
       else
         xi[0][q - 8] = d;
     }
     OMR_PHASE(pslot, hs, 1);
-    F::fwd<1, true>(xr, xi, xch, tws, lane, tb.fft1);
+    F::fwd<1, false>(xr, xi, xch, tws, lane);  // pass-0 twiddles from LDS (the lambda loses the
+                                               // global table's restrict: vector loads every step)
     wave_lds_fence();  // the spectrum's writes stay below the transform's exchange reads
 #pragma unroll
     for (int e = 0; e < 8; ++e) xch[e * 64 + lane] = make_double2(xr[0][e], xi[0][e]);
@@ -195,15 +202,13 @@ __device__ __forceinline__ void br1l_body(
         si[0][e] = v.y;
       }
       OMR_PHASE(pslot, hs, 5);
-      F::inv<1, true>(sr, si, xch, tws, lane, tb.fft1);
+      F::inv<1, false>(sr, si, xch, tws, lane);
       OMR_PHASE(pslot, hs, 6);
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
-        const double y = q < 8 ? sr[0][q] : si[0][q - 8], v = rint(y);  // exact (< 2^43)
-        rg.note(y, v);
-        ac[q] = Lvl1Int::canon(ac[q] + (int)red<Mod<1>>(v));
+        ac[q] = Lvl1Off::add(ac[q], Lvl1Off::round<G>(q < 8 ? sr[0][q] : si[0][q - 8], &rg));  // exact (< 2^43)
         ext[wave][acc_coef(lane, q)] = ac[q];
-        ext[wave][N1 + acc_coef(lane, q)] = -ac[q];
+        ext[wave][N1 + acc_coef(lane, q)] = Lvl1Off::neg(ac[q]);
       }
     }
     wg_barrier_lds();  // ACC staged for the next step's digits
@@ -230,13 +235,14 @@ __device__ __forceinline__ void br1l_body(
   rg.publish(margin);
   if (mode == 0) {  // extract_lwe_locally (coefficient 0), detector.rs:561
     uint32_t *o = ext_out + g * (N1 + 1);
-    for (int j = threadIdx.x; j < N1; j += 64 * W) o[j] = Lvl1Int::to_u32(j == 0 ? ext[0][0] : -ext[0][N1 - j]);
-    if (threadIdx.x == 0) o[N1] = Lvl1Int::to_u32(ext[1][0]);
+    for (int j = threadIdx.x; j < N1; j += 64 * W)
+      o[j] = Lvl1Int::to_u32(j == 0 ? Lvl1Off::dec(ext[0][0]) : -Lvl1Off::dec(ext[0][N1 - j]));
+    if (threadIdx.x == 0) o[N1] = Lvl1Int::to_u32(Lvl1Off::dec(ext[1][0]));
   } else {
     uint64_t *o = rlwe_out + g * 2 * N1;
     for (int j = threadIdx.x; j < N1; j += 64 * W) {
-      o[j] = Lvl1Int::to_u32(ext[0][j]);
-      o[N1 + j] = Lvl1Int::to_u32(ext[1][j]);
+      o[j] = Lvl1Int::to_u32(Lvl1Off::dec(ext[0][j]));
+      o[N1 + j] = Lvl1Int::to_u32(Lvl1Off::dec(ext[1][j]));
     }
   }
 }
@@ -280,6 +286,8 @@ __global__ __launch_bounds__(BR2L_T, 1) void br2l_kernel(const uint32_t *__restr
   __shared__ double tws[N + 136 * 5];  // forward twiddles + the five small-digit stage tables
   const int g = threadIdx.x / T, t = threadIdx.x % T;
   double *X = xbuf[g];
+  // pass-0 twiddles read from the LDS copy too (gt = tw): from the global table they were vector
+  // loads on every step's critical path (no restrict on DeviceTables' pointers, so no scalar loads)
   const double *tw = tws, *t0 = tws + N;
   const uint32_t *lwe = lwe_int + (size_t)blockIdx.x * (NI + 1);
   double acc[E];
@@ -331,9 +339,9 @@ __global__ __launch_bounds__(BR2L_T, 1) void br2l_kernel(const uint32_t *__restr
 #pragma unroll
         for (int e = 0; e < E; ++e) f[e] = DG::get_int(pk[e], k) + 64;
         if (h == 0)  // digits on X0, X1, X0, ...
-          NTT::template fwd_small<0>(f, t0, x, X, tw, t, tb.tw2c);
+          NTT::template fwd_small<0>(f, t0, x, X, tw, t, tw);
         else
-          NTT::template fwd_small<1>(f, t0, x, X, tw, t, tb.tw2c);
+          NTT::template fwd_small<1>(f, t0, x, X, tw, t, tw);
 #pragma unroll
         for (int e = 0; e < E; ++e) {
           accA[e] += mm<M>(x[e], cur.a[e]);
@@ -356,7 +364,7 @@ __global__ __launch_bounds__(BR2L_T, 1) void br2l_kernel(const uint32_t *__restr
     double s[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) s[e] = red<M>(red<M>(g == 0 ? accA[e] : accB[e]) + part[g][e * T + t]);
-    NTT::template inv<0>(s, X, tw, t, tb.tw2c);
+    NTT::template inv<0>(s, X, tw, t, tw);
 #pragma unroll
     for (int e = 0; e < E; ++e) acc[e] = canon<M>(acc[e] + s[e]);
   }
@@ -414,6 +422,8 @@ __global__ __launch_bounds__(BR2L_T, 1) void br2x_kernel(const uint32_t *__restr
   const int g = threadIdx.x / T, t = threadIdx.x % T;
   double *X = xbuf[g];
   double *ST = xbuf[0] + N;  // the staged accumulator (group 0's X1), read by both groups
+  // pass-0 twiddles read from the LDS copy too (gt = tw): from the global table they were vector
+  // loads on every step's critical path (no restrict on DeviceTables' pointers, so no scalar loads)
   const double *tw = tws, *t0 = tws + N;
   const uint32_t *lwe = lwe_int + (size_t)m * (NI + 1);
   double acc[E];  // ACC_r, group 0 only
@@ -472,9 +482,9 @@ __global__ __launch_bounds__(BR2L_T, 1) void br2x_kernel(const uint32_t *__restr
 #pragma unroll
       for (int e = 0; e < E; ++e) f[e] = DG::get_int(pk[e], k) + 64;
       if ((h & 1) == 0)
-        NTT::template fwd_small<0>(f, t0, x, X, tw, t, tb.tw2c);
+        NTT::template fwd_small<0>(f, t0, x, X, tw, t, tw);
       else
-        NTT::template fwd_small<1>(f, t0, x, X, tw, t, tb.tw2c);
+        NTT::template fwd_small<1>(f, t0, x, X, tw, t, tw);
 #pragma unroll
       for (int e = 0; e < E; ++e) {
         accA[e] += mm<M>(x[e], cur.a[e]);
@@ -526,7 +536,7 @@ __global__ __launch_bounds__(BR2L_T, 1) void br2x_kernel(const uint32_t *__restr
 #pragma unroll
       for (int e = 0; e < E; ++e)
         s[e] = red<M>(keep[e] + ld_sc1(xg + (((size_t)m * 2 + (1 - r)) * 2 + slot) * N + e * T + t));
-      NTT::template inv<0>(s, X, tw, t, tb.tw2c);
+      NTT::template inv<0>(s, X, tw, t, tw);
       OMR_PHASE(pslot, (int)hc, 6);
 #pragma unroll
       for (int e = 0; e < E; ++e) acc[e] = canon<M>(acc[e] + s[e]);

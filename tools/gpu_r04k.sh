@@ -1,0 +1,10 @@
+# br2f instruction diet A/B (base, buffer-descriptor key loads + signed digit fields, + peeled
+# first digit), twice; then single-message latency base vs b2 (br1l pass-0 twiddles from LDS).
+set -o pipefail
+out=gpurun_out/r04k
+mkdir -p $out
+rm -f gpurun_out/bench_variants.log
+tools/bench_variants.sh 16384 --no-e2e || exit 2
+tools/bench_variants.sh 16384 --no-e2e || exit 3
+cp gpurun_out/bench_variants.log $out/ab.log
+for v in base b2 base b2; do OMR_KEEP_DEVICE=1 OMR_GPU_LIB=$PWD/tfhe-omr_amd/build/var_$v.so timeout -k 10 120 python tools/latency_split.py 1 7 > $out/lat_$v.log 2>&1 && echo "$v $(cat $out/lat_$v.log | tr '\n' ' ')" >> $out/lat_ab.log || exit 5; done
