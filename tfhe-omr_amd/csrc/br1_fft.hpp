@@ -211,7 +211,7 @@ template <bool FIRST>
 __device__ __forceinline__ void br1f_row(const uint32_t (&pk)[16], int k, int q, int qtotal, double (&outr)[2][8],
                                          double (&outi)[2][8], double2 *xch, const double2 *tws,
                                          __amdgpu_buffer_rsrc_t rsrc, double2 *kbuf, int lane, uint32_t lane16,
-                                         int wave, const double2 *__restrict__ gtw) {
+                                         int wave, const double2 *__restrict__ gtw, const double2 *w3) {
   using F = Fft512;
   const bool more = q + 1 < qtotal;
   wg_barrier_lds();  // every wave has finished reading buffer (q + 1) & 1 (row q - 1)
@@ -222,7 +222,7 @@ __device__ __forceinline__ void br1f_row(const uint32_t (&pk)[16], int k, int q,
     xr[0][e] = Lvl1Int::digit(pk[e], k);
     xi[0][e] = Lvl1Int::digit(pk[8 + e], k);
   }
-  F::fwd<1, true>(xr, xi, xch, tws, lane, gtw);
+  F::fwd<1, true>(xr, xi, xch, tws, lane, gtw, w3);
   if (more)
     vm_wait_row_in_flight();  // row q landed (row q + 1 may stay in flight)
   else
@@ -253,19 +253,20 @@ template <bool G>
 __device__ __forceinline__ void br1f_step_lds(uint32_t (&ac)[2][16], double2 *xch, const double2 *tws, int a,
                                               __amdgpu_buffer_rsrc_t rsrc, int q0, int qtotal, double2 *kbuf,
                                               int lane, uint32_t lane16, int wave,
-                                              const double2 *__restrict__ gtw, RoundGuard<G> &rg) {
+                                              const double2 *__restrict__ gtw, const double2 *w3,
+                                              RoundGuard<G> &rg) {
   using F = Fft512;
   uint32_t pk[2][16];
   br1f_digits(ac, reinterpret_cast<uint32_t *>(xch), a, lane, pk);
   double outr[2][8], outi[2][8];
-  br1f_row<true>(pk[0], 0, q0, qtotal, outr, outi, xch, tws, rsrc, kbuf, lane, lane16, wave, gtw);
+  br1f_row<true>(pk[0], 0, q0, qtotal, outr, outi, xch, tws, rsrc, kbuf, lane, lane16, wave, gtw, w3);
 #pragma unroll 1
   for (int k = 1; k < D1; ++k)
-    br1f_row<false>(pk[0], k, q0 + k, qtotal, outr, outi, xch, tws, rsrc, kbuf, lane, lane16, wave, gtw);
+    br1f_row<false>(pk[0], k, q0 + k, qtotal, outr, outi, xch, tws, rsrc, kbuf, lane, lane16, wave, gtw, w3);
 #pragma unroll 1
   for (int k = 0; k < D1; ++k)
-    br1f_row<false>(pk[1], k, q0 + D1 + k, qtotal, outr, outi, xch, tws, rsrc, kbuf, lane, lane16, wave, gtw);
-  F::inv_pair<true>(outr, outi, xch, tws, lane, gtw);  // both outputs, interleaved
+    br1f_row<false>(pk[1], k, q0 + D1 + k, qtotal, outr, outi, xch, tws, rsrc, kbuf, lane, lane16, wave, gtw, w3);
+  F::inv_pair<true>(outr, outi, xch, tws, lane, gtw, w3);  // both outputs, interleaved
 #pragma unroll
   for (int o = 0; o < 2; ++o)
 #pragma unroll
@@ -320,6 +321,10 @@ __device__ __forceinline__ void br1f_body(
   }
   for (int j = threadIdx.x; j < NF; j += 64 * W) tws[j] = tb.fft1[j];
   __syncthreads();
+  // pass 3's two lane twiddles in registers for the whole rotation: 2 KB of LDS reads fewer per
+  // transform (LDS runs at ~60 % of its bandwidth here; 595 -> 591 ms per 16,384 messages,
+  // profiles/r04/br1f_w3_ab.log)
+  const double2 w3[2] = {tws[255 + lane], tws[255 + 64 + lane]};
   // every step runs (a = 0 gives zero digits and leaves ACC unchanged) so the waves share the
   // staged key rows; row 0 is issued before the loop
   const __amdgpu_buffer_rsrc_t rsrc = bsk1_rsrc(bskf);
@@ -329,7 +334,7 @@ __device__ __forceinline__ void br1f_body(
 #pragma unroll 1
   for (int i = 0; i < N0; ++i) {
     const int a = __builtin_amdgcn_readfirstlane(la[i]);
-    br1f_step_lds<G>(ac, xch, tws, a, rsrc, i * 2 * D1, N0 * 2 * D1, kbuf, lane, lane16, wave, tb.fft1, rg);
+    br1f_step_lds<G>(ac, xch, tws, a, rsrc, i * 2 * D1, N0 * 2 * D1, kbuf, lane, lane16, wave, tb.fft1, w3, rg);
   }
   rg.publish(margin);
   __syncthreads();

@@ -309,8 +309,9 @@ struct WgFft {
 
   // P3: stage 8, pairs (e, e + 4); register bit 1 selects the even-sibling twiddle, bit 0 the factor i
   template <int C>
-  __device__ static __forceinline__ void fwd2(double (&xr)[C][E], double (&xi)[C][E], const double2 *tws, int lane) {
-    const double2 W[2] = {tws[255 + lane], tws[255 + 64 + lane]};
+  __device__ static __forceinline__ void fwd2(double (&xr)[C][E], double (&xi)[C][E], const double2 *tws, int lane,
+                                              const double2 *w3 = nullptr) {
+    const double2 W[2] = {w3 ? w3[0] : tws[255 + lane], w3 ? w3[1] : tws[255 + 64 + lane]};
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const double2 w = W[(e >> 1) & 1];
@@ -328,8 +329,9 @@ struct WgFft {
     }
   }
   template <int C>
-  __device__ static __forceinline__ void inv2(double (&xr)[C][E], double (&xi)[C][E], const double2 *tws, int lane) {
-    const double2 W[2] = {tws[255 + lane], tws[255 + 64 + lane]};
+  __device__ static __forceinline__ void inv2(double (&xr)[C][E], double (&xi)[C][E], const double2 *tws, int lane,
+                                              const double2 *w3 = nullptr) {
+    const double2 W[2] = {w3 ? w3[0] : tws[255 + lane], w3 ? w3[1] : tws[255 + 64 + lane]};
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const double2 w = W[(e >> 1) & 1];
@@ -349,18 +351,20 @@ struct WgFft {
   }
 
   // C transforms at once (lds holds C * BUF complex)
-  // G: pass-0 twiddles from the global table gtw (must be non-null)
+  // G: pass-0 twiddles from the global table gtw (must be non-null); w3: pass 3's two twiddles of
+  // this lane held in registers by the caller (else read from tws)
   template <int C, bool G = false>
   __device__ static __forceinline__ void fwd(double (&xr)[C][E], double (&xi)[C][E], double2 *lds,
                                              const double2 *tws, int lane,
-                                             const double2 *__restrict__ gtw = nullptr) {
+                                             const double2 *__restrict__ gtw = nullptr,
+                                             const double2 *w3 = nullptr) {
     fwd8<0, C, G>(xr, xi, tws, lane, gtw);
     swap01<C>(xr, xi);
     fwd4<C>(xr, xi, tws, lane);
     exchange<C, 1, 2>(xr, xi, lds, lane);
     fwd8<2, C>(xr, xi, tws, lane);
     swap23<C>(xr, xi);
-    fwd2<C>(xr, xi, tws, lane);
+    fwd2<C>(xr, xi, tws, lane, w3);
   }
   template <int C, bool G = false>
   __device__ static __forceinline__ void inv(double (&xr)[C][E], double (&xi)[C][E], double2 *lds,
@@ -381,8 +385,9 @@ struct WgFft {
   template <bool G = false>
   __device__ static __forceinline__ void inv_pair(double (&xr)[2][E], double (&xi)[2][E], double2 *lds,
                                                   const double2 *tws, int lane,
-                                                  const double2 *__restrict__ gtw = nullptr) {
-    inv2<2>(xr, xi, tws, lane);
+                                                  const double2 *__restrict__ gtw = nullptr,
+                                                  const double2 *w3 = nullptr) {
+    inv2<2>(xr, xi, tws, lane, w3);
     swap23<2>(xr, xi);
     inv8<2, 2>(xr, xi, tws, lane);
 #pragma unroll
