@@ -1,0 +1,9 @@
+# Timing-only ablations of br2f_kernel (wrong results by construction): without the cross-wave
+# exchange barrier, and with output B's key blocks read from output A's (L1-hot) addresses; twice.
+set -o pipefail
+out=gpurun_out/r04s
+mkdir -p $out
+rm -f gpurun_out/bench_variants.log
+tools/bench_variants.sh 16384 --no-e2e || exit 2
+tools/bench_variants.sh 16384 --no-e2e || exit 3
+cp gpurun_out/bench_variants.log $out/ab.log
