@@ -1,4 +1,6 @@
 # br1f ablation 3 (restrict-preserving row function): base, buffer DMA + peel, without peel, without buffer DMA, + floor rounding and H/2 offset, + v_and_or addresses; twice.
+# (Record of a round-4 A/B: the var_*.so it times were built by tools/build_variant.sh from scratch
+# edits / -D switches that were folded into or removed from the sources afterwards)
 set -o pipefail
 out=gpurun_out/r04i
 mkdir -p $out
