@@ -1,7 +1,7 @@
 # br2f instruction diet A/B (base, buffer-descriptor key loads + signed digit fields, + peeled
+# first digit), twice; then single-message latency base vs b2 (br1l pass-0 twiddles from LDS).
 # (Record of a round-4 A/B: the var_*.so it times were built by tools/build_variant.sh from scratch
 # edits / -D switches that were folded into or removed from the sources afterwards)
-# first digit), twice; then single-message latency base vs b2 (br1l pass-0 twiddles from LDS).
 set -o pipefail
 out=gpurun_out/r04k
 mkdir -p $out

@@ -1,7 +1,7 @@
 # In-wave LDS exchanges without the lgkmcnt(0) park (OMR_LDS_INORDER=1): the full GPU suite on the
+# variant library, then base vs inorder timing twice and single-message latency.
 # (Record of a round-4 A/B: the var_*.so it times were built by tools/build_variant.sh from scratch
 # edits / -D switches that were folded into or removed from the sources afterwards)
-# variant library, then base vs inorder timing twice and single-message latency.
 set -o pipefail
 out=gpurun_out/r04o
 mkdir -p $out

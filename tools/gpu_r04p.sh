@@ -1,7 +1,7 @@
 # br1f pass-3 twiddles held in registers (OMR_BR1_W3REG): base vs w3, three times each; the parity
+# tests of the level-1 paths on w3.
 # (Record of a round-4 A/B: the var_*.so it times were built by tools/build_variant.sh from scratch
 # edits / -D switches that were folded into or removed from the sources afterwards)
-# tests of the level-1 paths on w3.
 set -o pipefail
 out=gpurun_out/r04p
 mkdir -p $out

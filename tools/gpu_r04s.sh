@@ -1,7 +1,7 @@
 # Timing-only ablations of br2f_kernel (wrong results by construction): without the cross-wave
+# exchange barrier, and with output B's key blocks read from output A's (L1-hot) addresses; twice.
 # (Record of a round-4 A/B: the var_*.so it times were built by tools/build_variant.sh from scratch
 # edits / -D switches that were folded into or removed from the sources afterwards)
-# exchange barrier, and with output B's key blocks read from output A's (L1-hot) addresses; twice.
 set -o pipefail
 out=gpurun_out/r04s
 mkdir -p $out
