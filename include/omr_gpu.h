@@ -54,7 +54,12 @@ typedef enum {
   OMR_ERR_INVALID_ARGUMENT = 1,
   OMR_ERR_DEVICE = 2,
   OMR_ERR_OUT_OF_MEMORY = 3,
-  OMR_ERR_NOT_INVERTIBLE = 4 /* OmrError::InvertibleMatrix, error.rs:5-8 */
+  OMR_ERR_NOT_INVERTIBLE = 4, /* OmrError::InvertibleMatrix, error.rs:5-8 */
+  /* A level-1 FFT external product of a detect call could not be certified exact: the key's a
+   * priori bound E1 is >= 0.5 and the call's observed rounding margin reached 1 - E1 (see
+   * omr_ctx_exactness). The outputs of that call are not guaranteed; the reference's products are
+   * exact for every key (concrete-ntt, omr_core/Cargo.toml:38-45). */
+  OMR_ERR_INEXACT = 5
 } omr_status;
 
 /* Message of the last failing call on this thread ("" if none). */
@@ -190,6 +195,17 @@ omr_status omr_ctx_check(omr_ctx *ctx, void *hip_stream);
 omr_status omr_ctx_set_rounding_guard(omr_ctx *ctx, int enable);
 omr_status omr_ctx_rounding_margin(omr_ctx *ctx, double observed[2], double apriori[2],
                                    double kappa[2], int reset);
+/* The exactness contract. A level whose a priori bound E >= 0.5 runs its guarded
+ * kernels on EVERY launch of the context, whatever omr_ctx_set_rounding_guard says; after each
+ * such launch the observed margin m of that launch is compared with 1 - E on the device:
+ *  - level 2: a launch with m >= 1 - E2 is re-run on the exact modular NTT (the latency family's
+ *    br2l_kernel + trace), in the same stream order, so its outputs are exact;
+ *  - level 1: a launch with m >= 1 - E1 marks the context; the host entry points, omr_ctx_check and
+ *    the next detect call report it as OMR_ERR_INEXACT (and clear it).
+ * guarded[l] != 0 when level l + 1 is guarded on every launch (automatically or by the user);
+ * breaches[l] counts the launches of level l + 1 whose margin reached the threshold. Any pointer
+ * may be NULL. Reading breaches synchronises the device. */
+omr_status omr_ctx_exactness(omr_ctx *ctx, int guarded[2], uint64_t breaches[2]);
 /* Diagnostics: `count` stored key-spectrum values (complex, re/im pairs) starting at value `first`
  * of level 1 (BSK1, [512][8][2][512], /512) or level 2 (BSK2 limbs, [670][12][2][2][1024], /1024),
  * in the kernels' storage order (register-major slots). */

@@ -32,6 +32,8 @@ pub mod ffi {
     pub const OMR_ERR_DEVICE: OmrStatus = 2;
     pub const OMR_ERR_OUT_OF_MEMORY: OmrStatus = 3;
     pub const OMR_ERR_NOT_INVERTIBLE: OmrStatus = 4;
+    /// a level-1 FFT product of a detect call could not be certified exact (omr_ctx_exactness)
+    pub const OMR_ERR_INEXACT: OmrStatus = 5;
 
     pub const OMR_N0: usize = 512;
     pub const OMR_Q0: u32 = 2048;
@@ -145,6 +147,7 @@ pub mod ffi {
         pub fn omr_ctx_set_rounding_guard(ctx: *mut OmrCtx, enable: c_int) -> OmrStatus;
         pub fn omr_ctx_rounding_margin(ctx: *mut OmrCtx, observed: *mut f64, apriori: *mut f64, kappa: *mut f64,
                                        reset: c_int) -> OmrStatus;
+        pub fn omr_ctx_exactness(ctx: *mut OmrCtx, guarded: *mut c_int, breaches: *mut u64) -> OmrStatus;
         pub fn omr_fft_twiddles_dd(level: c_int, out: *mut f64) -> OmrStatus;
         pub fn omr_ctx_key_spectrum(ctx: *mut OmrCtx, level: c_int, first: usize, count: usize,
                                     out: *mut f64) -> OmrStatus;
@@ -489,6 +492,15 @@ impl GpuDetector {
             omr_ctx_rounding_margin(self.ctx, obs.as_mut_ptr(), apr.as_mut_ptr(), std::ptr::null_mut(), reset as c_int)
         })?;
         Ok((obs, apr))
+    }
+
+    /// The exactness contract (`omr_ctx_exactness`): (guarded on every launch, breaching launches)
+    /// per level. A level whose a priori bound is >= 0.5 is guarded automatically; a level-2 breach
+    /// was re-run on the exact NTT, a level-1 breach surfaced as `OMR_ERR_INEXACT`.
+    pub fn exactness(&self) -> Result<([bool; 2], [u64; 2]), OmrError> {
+        let (mut g, mut b) = ([0 as c_int; 2], [0u64; 2]);
+        check(unsafe { omr_ctx_exactness(self.ctx, g.as_mut_ptr(), b.as_mut_ptr()) })?;
+        Ok(([g[0] != 0, g[1] != 0], b))
     }
 
     /// Chunks of at most `max_messages` messages run the latency kernels (0 = never).

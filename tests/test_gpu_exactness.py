@@ -208,3 +208,66 @@ def test_handoff_buffers_mixed_sizes():
     det.check()
     det.close()
     ref.close()
+
+
+# ---- the exactness contract -----------------------------------------------
+def test_high_kappa_key_guarded_and_oracle_exact():
+    """A key whose a priori bound E2 is >= 1 (tests/crafted_keys.py: aligned maximal level-2 limbs on
+    four steps): the context guards level 2 on every launch without being asked, every such launch
+    breaches the threshold 1 - E2 <= 0 and is re-run on the exact NTT (br2l_fallback_kernel +
+    trace_fallback_kernel), and the outputs equal the oracle's -- fused trace (timing off) and the
+    split trace (detect_with_time_info) alike, and the level-2 stage entry."""
+    import crafted_keys as CK
+    import oracle_lib as O
+    _, _, dk = PL.keys()
+    ck = A.DetectionKey(dk.bsk1, dk.ksk, CK.high_kappa_bsk2(dk.bsk2), dk.trace_key)
+    det = A.Detector(ck)
+    try:
+        m = det.rounding_margin()
+        assert m["apriori"][0] < 0.5 <= 1.0 <= m["apriori"][1], m
+        from fft_bound import apriori_bounds
+        e1, e2, _, _ = apriori_bounds(ck)
+        assert abs(m["apriori"][1] - e2) < 1e-9 * e2
+        ex = det.exactness()
+        assert ex == {"guarded": [False, True], "breaches": [0, 0]}, ex
+        det.set_latency_threshold(0)  # throughput kernels: the FFT level 2
+        mask = np.arange(72) % 9 == 0
+        ca, cb = PL.mixed_clues(mask, seed=77)
+        got = det.detect_batch(ca, cb)
+        ex = det.exactness()
+        assert ex["guarded"] == [False, True] and ex["breaches"][0] == 0 and ex["breaches"][1] >= 1, ex
+        got_split, _ = det.detect_with_time_info(ca[:40], cb[:40])
+        assert det.exactness()["breaches"][1] > ex["breaches"][1]
+        orc = O.OracleDetector(ck.bsk1, ck.ksk, ck.bsk2, ck.trace_key)
+        try:
+            ref = orc.detect_batch(ca, cb)
+            lwe = np.stack([orc.first_level(ca[i], cb[i]) for i in range(8)])
+            ref_rot = np.stack([orc.br2(x) for x in lwe])
+        finally:
+            orc.close()
+        assert np.array_equal(got, ref), "guarded high-kappa detect differs from the oracle"
+        assert np.array_equal(got_split, ref[:40]), "split-trace path differs from the oracle"
+        assert np.array_equal(det.blind_rotate_level2(lwe), ref_rot), "level-2 rotation entry differs"
+        det.check()
+    finally:
+        det.close()
+
+
+@pytest.mark.parametrize("pack_seed,key_seed", [(42, 8), (43, 7), (4242, 11)])
+def test_apriori_bound_below_half_on_gpu_generated_keys(pack_seed, key_seed):
+    """Three more GPU-generated keys: both bounds below 0.5, so no launch needs the guard."""
+    import torch
+    dev = torch.device("cuda", 0)
+    pack = A.SecretKeyPack(pack_seed)
+    bufs = [torch.empty(int(np.prod(shape)), dtype=dt, device=dev)
+            for shape, dt in ((A.BSK1_SHAPE, torch.int32), (A.KSK_SHAPE, torch.int32),
+                              (A.BSK2_SHAPE, torch.int64), (A.TK_SHAPE, torch.int64))]
+    pack.generate_detection_key_device(key_seed, *[b.data_ptr() for b in bufs])
+    det = A.Detector.from_device_key(*[b.data_ptr() for b in bufs])
+    try:
+        apr = det.rounding_margin()["apriori"]
+        print(f"\npack {pack_seed} key {key_seed}: E1 {apr[0]:.4f}, E2 {apr[1]:.4f}")
+        assert apr[0] < 0.5 and apr[1] < 0.5, apr
+        assert det.exactness() == {"guarded": [False, False], "breaches": [0, 0]}
+    finally:
+        det.close()

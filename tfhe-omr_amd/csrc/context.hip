@@ -278,12 +278,14 @@ struct omr_ctx {
   size_t t_cap = 0;
   int num_cu = 0;
   bool coop = false;  // hipDeviceAttributeCooperativeLaunch
-  // rounding-margin guard (exactness.hpp): guarded kernel variants when on; margin[0] level 1,
-  // margin[1] level 2 (bits of the largest |y - rint(y)|); kappa: largest stored key spectrum
-  // magnitude per level; apriori: the bound it gives (apriori_bound)
-  bool guard = false;
+  // rounding-margin guard (exactness.hpp): guarded kernel variants for level l when the user set
+  // the guard or the key's a priori bound E_l >= 0.5 (guard_auto, the exactness contract); margin:
+  // the GUARD_WORDS guard words (bits of the largest |y - rint(y)|, per launch and cumulative, and
+  // the breach counts); kappa: largest stored key spectrum magnitude per level; apriori: the bound it
+  // gives (apriori_bound); thr = 1 - apriori, the certificate threshold of one launch
+  bool guard = false, guard_auto[2] = {false, false};
   unsigned long long *margin = nullptr;
-  double kappa[2] = {0.0, 0.0}, apriori[2] = {0.0, 0.0};
+  double kappa[2] = {0.0, 0.0}, apriori[2] = {0.0, 0.0}, thr[2] = {1.0, 1.0};
   // host-API staging
   uint16_t *s_clue_a = nullptr, *s_clue_b = nullptr;
   uint64_t *s_out = nullptr;
@@ -329,6 +331,8 @@ struct omr_ctx {
 #define OMR_BR2_NAME "br2f_kernel"
 
 namespace {
+
+bool guarded(const omr_ctx *c, int level) { return c->guard || c->guard_auto[level]; }
 
 // Frees a device allocation made by this library (a failure here leaves nothing to recover).
 template <typename T>
@@ -475,14 +479,36 @@ bool latency_path(const omr_ctx *c, size_t n) { return n <= c->latency_max; }
 // reports (and clears) an error whose copy has landed: callers sync the stream first for a
 // definitive answer (omr_ctx_check, the host entry points), or call it before enqueueing new work
 // (the device entry points) so a failed earlier call is never attributed to a later one.
+// The same word carries GUARD_ERR_INEXACT: a guarded level-1 launch whose rounding margin reached
+// the certificate threshold (guard_fold_kernel), reported as OMR_ERR_INEXACT.
 omr_status take_handoff_error(omr_ctx *c) {
   if (!c->x_err_host || !__atomic_load_n(c->x_err_host, __ATOMIC_ACQUIRE)) return OMR_OK;
   HIP_TRY(hipDeviceSynchronize());  // no launch may still be copying the flag
-  __atomic_store_n(c->x_err_host, 0, __ATOMIC_RELEASE);
+  const int bits = __atomic_exchange_n(c->x_err_host, 0, __ATOMIC_ACQ_REL);
   HIP_TRY(hipMemset(c->x_err, 0, sizeof(int)));
-  return set_error(OMR_ERR_DEVICE,
-                   "level-2 two-CU hand-off timed out: the output of an earlier detect call on this "
-                   "context is invalid");
+  if (bits & GUARD_ERR_HANDOFF)
+    return set_error(OMR_ERR_DEVICE,
+                     "level-2 two-CU hand-off timed out: the output of an earlier detect call on this "
+                     "context is invalid");
+  return set_error(OMR_ERR_INEXACT,
+                   "a level-1 FFT external product of an earlier detect call on this context could not "
+                   "be certified exact (key a priori bound E1 >= 0.5 and margin >= 1 - E1): its output "
+                   "is not guaranteed");
+}
+
+// Zero the per-launch guard word of `level` before a guarded launch.
+omr_status guard_begin(omr_ctx *c, int level, hipStream_t st) {
+  HIP_TRY(hipMemsetAsync(c->margin + 2 + level, 0, sizeof(unsigned long long), st));
+  return OMR_OK;
+}
+// After a guarded launch (and, for level 2, its conditional exact re-run): fold the launch's margin
+// into the cumulative word, count a breach, and (level 1) raise the context's error word, which is
+// copied to the pinned host word like the hand-off timeout.
+omr_status guard_end(omr_ctx *c, int level, hipStream_t st) {
+  guard_fold_kernel<<<1, 64, 0, st>>>(c->margin, level, c->thr[level], c->x_err);
+  HIP_TRY(hipGetLastError());
+  if (level == 0) HIP_TRY(hipMemcpyAsync(c->x_err_host, c->x_err, sizeof(int), hipMemcpyDeviceToHost, st));
+  return OMR_OK;
 }
 
 // LWE key switch + modulus switch of B messages (lwe1t [1025][B] -> out [B][671]). Up to 64
@@ -506,19 +532,23 @@ omr_status launch_br1(omr_ctx *c, size_t n, const uint16_t *ca, const uint16_t *
                       const uint16_t *la, const uint16_t *lb, uint32_t *ext, uint64_t *rlwe, int mode,
                       hipStream_t st, size_t msgs) {
   const unsigned g1 = (unsigned)((n + BR1F_WPG - 1) / BR1F_WPG);
+  const bool g = guarded(c, 0);
+  omr_status s;
+  if (g && (s = guard_begin(c, 0, st)) != OMR_OK) return s;
   if (latency_path(c, msgs)) {
-    if (c->guard)
+    if (g)
       br1l_guard_kernel<<<(unsigned)n, 64 * BR1L_WAVES, 0, st>>>(ca, cb, la, lb, c->bsk1l, c->tb, ext, rlwe, mode,
-                                                                  c->margin);
+                                                                  c->margin + 2);
     else
       br1l_kernel<<<(unsigned)n, 64 * BR1L_WAVES, 0, st>>>(ca, cb, la, lb, c->bsk1l, c->tb, ext, rlwe, mode);
-  } else if (c->guard) {
-    br1f_guard_kernel<<<g1, 64 * BR1F_WPG, 0, st>>>(ca, cb, la, lb, c->bsk1f, c->tb, ext, rlwe, mode, n, c->margin);
+  } else if (g) {
+    br1f_guard_kernel<<<g1, 64 * BR1F_WPG, 0, st>>>(ca, cb, la, lb, c->bsk1f, c->tb, ext, rlwe, mode, n,
+                                                    c->margin + 2);
   } else {
     br1f_kernel<<<g1, 64 * BR1F_WPG, 0, st>>>(ca, cb, la, lb, c->bsk1f, c->tb, ext, rlwe, mode, n);
   }
   HIP_TRY(hipGetLastError());
-  return OMR_OK;
+  return g ? guard_end(c, 0, st) : OMR_OK;
 }
 
 // br2x_kernel over 2 n workgroups as a cooperative launch (co-residency guaranteed, or the launch
@@ -536,12 +566,6 @@ omr_status launch_br2x(omr_ctx *c, size_t n, const uint32_t *lwe_int, uint64_t *
     HIP_TRY(hipMalloc(&c->x_slots, n * 4 * N2 * sizeof(double)));
     HIP_TRY(hipMalloc(&c->x_flags, n * 2 * sizeof(uint32_t)));
     c->x_cap = n;
-  }
-  if (!c->x_err) {
-    HIP_TRY(hipMalloc(&c->x_err, sizeof(int)));
-    HIP_TRY(hipMemset(c->x_err, 0, sizeof(int)));
-    HIP_TRY(hipHostMalloc((void **)&c->x_err_host, sizeof(int), hipHostMallocDefault));
-    *c->x_err_host = 0;
   }
   HIP_TRY(hipMemsetAsync(c->x_flags, 0, n * 2 * sizeof(uint32_t), st));
   const double *bsk2 = c->bsk2;
@@ -578,12 +602,6 @@ omr_status launch_trace_x(omr_ctx *c, size_t n, uint64_t *io, hipStream_t st, bo
     HIP_TRY(hipMalloc(&c->t_flags, n * TRACE_X * sizeof(uint32_t)));
     c->t_cap = n;
   }
-  if (!c->x_err) {
-    HIP_TRY(hipMalloc(&c->x_err, sizeof(int)));
-    HIP_TRY(hipMemset(c->x_err, 0, sizeof(int)));
-    HIP_TRY(hipHostMalloc((void **)&c->x_err_host, sizeof(int), hipHostMallocDefault));
-    *c->x_err_host = 0;
-  }
   HIP_TRY(hipMemsetAsync(c->t_flags, 0, n * TRACE_X * sizeof(uint32_t), st));
   const double *tk = c->tk;
   DeviceTables tb = c->tb;
@@ -616,11 +634,23 @@ omr_status launch_br2(omr_ctx *c, size_t n, const uint32_t *lwe_int, uint64_t *o
     split_trace = true;
   } else {
     const int m = split_trace && mode == 0 ? 1 : mode;
-    if (c->guard)
+    if (guarded(c, 1)) {
+      // the exactness contract: a launch whose margin reaches 1 - E2 is re-run on the exact NTT
+      // (br2l_fallback_kernel: every workgroup leaves at once otherwise), its trace too when fused
+      omr_status s;
+      if ((s = guard_begin(c, 1, st)) != OMR_OK) return s;
       br2f_guard_kernel<<<(unsigned)n, Fft1024::T, 0, st>>>(lwe_int, c->bsk2f, c->fft2, c->tk, c->tb, out, m,
-                                                            c->margin + 1);
-    else
+                                                            c->margin + 3);
+      HIP_TRY(hipGetLastError());
+      br2l_fallback_kernel<<<(unsigned)n, BR2L_T, 0, st>>>(lwe_int, c->bsk2, c->tb, out, c->margin + 3, c->thr[1]);
+      HIP_TRY(hipGetLastError());
+      if (m == 0)
+        trace_fallback_kernel<<<(unsigned)n, BR2_T, 0, st>>>(out, c->tk, c->tb, c->margin + 3, c->thr[1]);
+      HIP_TRY(hipGetLastError());
+      if ((s = guard_end(c, 1, st)) != OMR_OK) return s;
+    } else {
       br2f_kernel<<<(unsigned)n, Fft1024::T, 0, st>>>(lwe_int, c->bsk2f, c->fft2, c->tk, c->tb, out, m);
+    }
   }
   HIP_TRY(hipGetLastError());
   if (mid) HIP_TRY(hipEventRecord(mid, st));
@@ -676,6 +706,11 @@ extern "C" omr_status omr_ctx_create(const omr_detection_key_view *key, int devi
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&c->scratch_free, hipEventDisableTiming) != hipSuccess)
     return fail(set_error(OMR_ERR_DEVICE, "hipStreamCreate / hipEventCreate failed"));
+  // the context's error word (hand-off timeout, uncertified level-1 product) and its pinned copy
+  if (hipMalloc(&c->x_err, sizeof(int)) != hipSuccess || hipMemset(c->x_err, 0, sizeof(int)) != hipSuccess ||
+      hipHostMalloc((void **)&c->x_err_host, sizeof(int), hipHostMallocDefault) != hipSuccess)
+    return fail(set_error(OMR_ERR_OUT_OF_MEMORY, "omr_ctx_create: error word"));
+  *c->x_err_host = 0;
   // tables
   std::vector<double> tw1, itw1, tw2, itw2;
   twiddles(Q1, N1, 7, tw1, itw1);
@@ -754,10 +789,10 @@ extern "C" omr_status omr_ctx_create(const omr_detection_key_view *key, int devi
   {  // kappa_r per key row (the a priori bound's key constants) and the guard's margin words
     const size_t rows1 = BSK1_ELEMS / 2 / Fft512::N, rows2 = BSK2_ELEMS / Fft1024::n;
     DevBufHost<double> km;
-    if (hipMalloc(&c->margin, 2 * sizeof(unsigned long long)) != hipSuccess ||
+    if (hipMalloc(&c->margin, GUARD_WORDS * sizeof(unsigned long long)) != hipSuccess ||
         hipMalloc(&km.p, (rows1 + rows2) * sizeof(double)) != hipSuccess)
       return fail(set_error(OMR_ERR_OUT_OF_MEMORY, "omr_ctx_create: margin words"));
-    const bool ok = hipMemsetAsync(c->margin, 0, 2 * sizeof(unsigned long long), c->stream) == hipSuccess;
+    const bool ok = hipMemsetAsync(c->margin, 0, GUARD_WORDS * sizeof(unsigned long long), c->stream) == hipSuccess;
     if (ok) {
       row_max_abs_kernel<<<(unsigned)rows1, 256, 0, c->stream>>>(c->bsk1f, Fft512::N, km.p);
       row_max_abs_kernel<<<(unsigned)rows2, 256, 0, c->stream>>>(c->bsk2f, Fft1024::n, km.p + rows1);
@@ -771,6 +806,12 @@ extern "C" omr_status omr_ctx_create(const omr_detection_key_view *key, int devi
     c->kappa[1] = *std::max_element(k2.begin(), k2.end());
     c->apriori[0] = apriori_bound(1, k1);
     c->apriori[1] = apriori_bound(2, k2);
+    // the exactness contract: a level whose bound does not prove every rounding exact is guarded
+    // on every launch and checked against 1 - E (omr_ctx_exactness)
+    for (int l = 0; l < 2; ++l) {
+      c->guard_auto[l] = !(c->apriori[l] < 0.5);
+      c->thr[l] = 1.0 - c->apriori[l];
+    }
   }
   if ((st = convert_keys<2, uint64_t, double>(key->trace_key, TK_ELEMS / N2, c->tk, 1.0, c->tb.tw2,
                                               c->stream)) != OMR_OK)
@@ -882,6 +923,22 @@ extern "C" omr_status omr_ctx_rounding_margin(omr_ctx *c, double observed[2], do
     if (kappa) kappa[l] = c->kappa[l];
   }
   if (reset) HIP_TRY(hipMemset(c->margin, 0, 2 * sizeof(unsigned long long)));
+  return OMR_OK;
+}
+
+extern "C" omr_status omr_ctx_exactness(omr_ctx *c, int guarded_out[2], uint64_t breaches[2]) {
+  if (!c) return set_error(OMR_ERR_INVALID_ARGUMENT, "omr_ctx_exactness: NULL ctx");
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (guarded_out)
+    for (int l = 0; l < 2; ++l) guarded_out[l] = guarded(c, l) ? 1 : 0;
+  if (breaches) {
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipDeviceSynchronize());
+    unsigned long long w[2];
+    HIP_TRY(hipMemcpy(w, c->margin + 4, sizeof(w), hipMemcpyDeviceToHost));
+    breaches[0] = w[0];
+    breaches[1] = w[1];
+  }
   return OMR_OK;
 }
 
@@ -1320,7 +1377,7 @@ extern "C" omr_status omr_first_level(omr_ctx *c, const uint16_t *ca, const uint
   HIP_TRY(hipMemcpyAsync(lwe_int, c->lwe_int, D * (NI + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   if ((s = scratch_release(c, st)) != OMR_OK) return s;
   HIP_TRY(hipStreamSynchronize(st));
-  return OMR_OK;
+  return take_handoff_error(c);  // an uncertified level-1 product (the exactness contract)
 }
 
 extern "C" omr_status omr_fft1_mul(omr_ctx *c, const uint32_t *a, const uint32_t *k, size_t n,
@@ -1359,6 +1416,7 @@ extern "C" omr_status omr_blind_rotate_level1(omr_ctx *c, const uint16_t *la, co
   omr_status s = launch_br1(c, n, nullptr, nullptr, da.p, db.p, nullptr, dout.p, 1, c->stream, n);
   if (s != OMR_OK) return s;
   HIP_TRY(hipStreamSynchronize(c->stream));
+  if ((s = take_handoff_error(c)) != OMR_OK) return s;
   HIP_TRY(hipMemcpy(out, dout.p, n * 2 * N1 * sizeof(uint64_t), hipMemcpyDeviceToHost));
   return OMR_OK;
 }

@@ -274,9 +274,8 @@ __global__ __launch_bounds__(64 * BR1L_WAVES, 1) void br1l_guard_kernel(
 // coefficient domain, u64 [2][N2] (mode 1 of br2f_kernel); trace_kernel finishes mode 0.
 constexpr int BR2L_T = 2 * BR2_T;
 
-__global__ __launch_bounds__(BR2L_T, 1) void br2l_kernel(const uint32_t *__restrict__ lwe_int,
-                                                         const double *__restrict__ bsk2, DeviceTables tb,
-                                                         uint64_t *__restrict__ out) {
+__device__ __forceinline__ void br2l_body(const uint32_t *__restrict__ lwe_int, const double *__restrict__ bsk2,
+                                          DeviceTables tb, uint64_t *__restrict__ out) {
   using M = Mod<2>;
   constexpr int T = BR2_T, E = BR2_E, N = N2;
   using NTT = CmuxNtt;
@@ -371,6 +370,24 @@ __global__ __launch_bounds__(BR2L_T, 1) void br2l_kernel(const uint32_t *__restr
   uint64_t *o = out + (size_t)blockIdx.x * 2 * N + (size_t)g * N;
 #pragma unroll
   for (int e = 0; e < E; ++e) o[t + e * T] = to_u64<M>(acc[e]);
+}
+__global__ __launch_bounds__(BR2L_T, 1) void br2l_kernel(const uint32_t *__restrict__ lwe_int,
+                                                         const double *__restrict__ bsk2, DeviceTables tb,
+                                                         uint64_t *__restrict__ out) {
+  br2l_body(lwe_int, bsk2, tb, out);
+}
+// The exact fallback of a guarded throughput level-2 launch (context.hip, launch_br2): the same
+// rotation on the modular NTT, run only when that launch's observed rounding margin reached the
+// certificate threshold 1 - E2 (every workgroup reads the word and leaves otherwise).
+__device__ __forceinline__ bool margin_breached(const unsigned long long *word, double thr) {
+  return __longlong_as_double((long long)*word) >= thr;
+}
+__global__ __launch_bounds__(BR2L_T, 1) void br2l_fallback_kernel(const uint32_t *__restrict__ lwe_int,
+                                                                  const double *__restrict__ bsk2, DeviceTables tb,
+                                                                  uint64_t *__restrict__ out,
+                                                                  const unsigned long long *lmargin, double thr) {
+  if (!margin_breached(lmargin, thr)) return;
+  br2l_body(lwe_int, bsk2, tb, out);
 }
 
 // ---- level 2 over two CUs per message --------------------------------------------------------
@@ -557,8 +574,7 @@ __global__ __launch_bounds__(BR2L_T, 1) void br2x_kernel(const uint32_t *__restr
 
 // hom_trace (detector.rs:626-639) in place on blind-rotation outputs (coefficient domain,
 // canonical u64 [2][N2] per message) -> NttRlweCiphertext u64 [2][N2].
-__global__ __launch_bounds__(BR2_T, 2) void trace_kernel(uint64_t *__restrict__ io, const double *__restrict__ tk,
-                                                         DeviceTables tb) {
+__device__ __forceinline__ void trace_body(uint64_t *__restrict__ io, const double *__restrict__ tk, DeviceTables tb) {
   using M = Mod<2>;
   constexpr int T = BR2_T, E = BR2_E, N = N2;
   using NTT = WgNtt<M, T, E>;
@@ -576,6 +592,17 @@ __global__ __launch_bounds__(BR2_T, 2) void trace_kernel(uint64_t *__restrict__ 
   }
   __syncthreads();
   hom_trace_store(acc0, acc1, xch, tws, xch + 2 * N, tk, tb, o, tid);
+}
+__global__ __launch_bounds__(BR2_T, 2) void trace_kernel(uint64_t *__restrict__ io, const double *__restrict__ tk,
+                                                         DeviceTables tb) {
+  trace_body(io, tk, tb);
+}
+// trace of br2l_fallback_kernel's output (same condition)
+__global__ __launch_bounds__(BR2_T, 2) void trace_fallback_kernel(uint64_t *__restrict__ io, const double *__restrict__ tk,
+                                                                  DeviceTables tb, const unsigned long long *lmargin,
+                                                                  double thr) {
+  if (!margin_breached(lmargin, thr)) return;
+  trace_body(io, tk, tb);
 }
 
 

@@ -85,6 +85,7 @@ EXPORTS = {
     "omr_ctx_check": (C.c_int, [C.c_void_p, C.c_void_p]),
     "omr_ctx_set_rounding_guard": (C.c_int, [C.c_void_p, C.c_int]),
     "omr_ctx_rounding_margin": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]),
+    "omr_ctx_exactness": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     "omr_fft_twiddles_dd": (C.c_int, [C.c_int, np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS")]),
     "omr_ctx_key_spectrum": (C.c_int, [C.c_void_p, C.c_int, C.c_size_t, C.c_size_t,
                                        np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS")]),
@@ -488,6 +489,14 @@ class Detector:
         obs, apr, kap = (C.c_double * 2)(), (C.c_double * 2)(), (C.c_double * 2)()
         _check(lib().omr_ctx_rounding_margin(self._h, obs, apr, kap, int(bool(reset))), "omr_ctx_rounding_margin")
         return {"observed": list(obs), "apriori": list(apr), "kappa": list(kap)}
+
+    def exactness(self) -> dict:
+        """The exactness contract (omr_ctx_exactness): {"guarded": [l1, l2] guarded on every launch
+        (automatically when the key's a priori bound E >= 0.5), "breaches": [l1, l2] launches whose
+        margin reached 1 - E (level 2: re-run on the exact NTT; level 1: OMR_ERR_INEXACT)}."""
+        g, b = (C.c_int * 2)(), (C.c_uint64 * 2)()
+        _check(lib().omr_ctx_exactness(self._h, g, b), "omr_ctx_exactness")
+        return {"guarded": [bool(v) for v in g], "breaches": list(b)}
 
     def key_spectrum(self, level: int, first: int, count: int) -> np.ndarray:
         """Stored key-spectrum values [count] complex (omr_ctx_key_spectrum)."""
