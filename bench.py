@@ -47,6 +47,14 @@ KERNEL_BYTES = {  # per message, per pipeline stage (kernel names from A.detect_
     "ks": KS_BYTES + 1025 * 4 + 671 * 4,
     "br2": BR2_BYTES + TRACE_BYTES + 671 * 4 + 2 * 2048 * 8,
 }
+# Compulsory HBM bytes: what a detect step must move at least. The device-resident
+# key forms are read once per launch: BSK1 FFT form 64 MiB, KSK int8 limbs 84 MiB, BSK2 FFT form
+# 503 MiB, trace key 8.6 MiB; per message the clue in, the pertinency ciphertext out and the
+# chunk scratch written and read back once (extracted LWEs u32 [7][1025], [1025], [671]).
+DEVICE_KEY_BYTES = 512 * 8 * 2 * 512 * 16 + 1024 * 4 * 672 * 32 + 670 * 12 * 4 * 1024 * 16 + 11 * 25 * 2 * 2048 * 8
+IO_BYTES_PER_MSG = 512 * 2 + 7 * 2 + 2 * 2048 * 8
+SCRATCH_BYTES_PER_MSG = 2 * 4 * (7 * 1025 + 1025 + 671)
+DETECT_KERNEL_ROLES = ("br1", "ks", "br2")
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
 # FP64 VALU peak: 256 CUs x 4 SIMDs x 16 FP64 FMA lanes x 2 FLOP x 2.4 GHz = 78.6 TFLOP/s (a wave64
 # FP64 instruction issues in 4 cycles); the arithmetic microbenchmark reaches 95 % of it
@@ -73,6 +81,9 @@ def parse():
     ap.add_argument("--cpu-msgs-per-thread", type=int, default=4, help="CPU baseline: all-core sample per thread")
     ap.add_argument("--force-dist", action="store_true",
                     help="initialise the RCCL process group even at world size 1 (rehearses the N > 1 path)")
+    ap.add_argument("--one-device", action="store_true",
+                    help="rehearsal of the N > 1 path on a one-GPU box: every rank uses device 0 and the "
+                         "process group is gloo (RCCL cannot run two ranks on one GPU); not a scaling number")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-latency", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the encode + reduce + retrieval pass")
@@ -166,25 +177,44 @@ def synthetic_payloads(first: int, count: int) -> np.ndarray:
     return ((h >> np.uint64(24)) & np.uint64(255)).astype(np.uint16)
 
 
-def rooflines(role, dom, launches, per_launch_msgs, launch_ms_total, value, world):
+def rooflines(role, dom, launches, per_launch_msgs, launch_ms_total, value, world, names):
     """Dominant-kernel rooflines from HIP-event launch times and committed counter summaries.
     The blind rotations are VALU-issue and latency bound: `roofline` prices the
     kernel's FP64 FLOPs per launch (counted per message by rocprofv3 SQ_INSTS_VALU_*_F64, FMA = 2)
     against the 78.6 TFLOP/s FP64 peak, and carries the fractions of the VALU issue slots used by
     its FP64 instructions and by all its VALU instructions (the level-2 FFT does 40 % fewer FLOPs
-    than round 2's NTT in 6 % less time, so its FLOP fraction is lower). `hbm` gives the key-streaming figure of SURVEY.md §8(d) (every key
-    byte counted once per message: the north-star "fraction of HBM roofline") next to the HBM
-    bytes the counters measured (FETCH_SIZE x 2 per the gfx950 correction + WRITE_SIZE)."""
+    than round 2's NTT in 6 % less time, so its FLOP fraction is lower). FP64 issue is the binding
+    roofline. `hbm` reports HBM honestly: the compulsory bytes of a step and
+    the bytes the counters measured (FETCH_SIZE x 2 per the gfx950 correction + WRITE_SIZE), each
+    against the 8 TB/s peak, and -- with no fraction, it is not a roofline -- SURVEY.md §8(d)'s
+    key-streaming figure (every key byte counted once per message), an effective rate of a batched
+    kernel whose concurrent workgroups share every key row through L2."""
     avg_launch_s = launch_ms_total / 1e3 / launches
     pmc, comp = load_profile("pmc_latest.json"), load_profile("compute_latest.json")
     traffic = None
     if pmc and dom in pmc.get("kernels", {}) and pmc.get("messages_per_launch"):
         traffic = pmc["kernels"][dom]["hbm_bytes_per_launch"] * per_launch_msgs / pmc["messages_per_launch"]
     key_stream = KERNEL_BYTES[role] * per_launch_msgs / avg_launch_s / 1e9
-    hbm = {"key_stream_equiv_GBps": round(key_stream, 1), "key_stream_frac": round(key_stream / HBM_PEAK_GBS, 4),
-           "measured_GBps": None if traffic is None else round(traffic / avg_launch_s / 1e9, 1),
-           "measured_frac": None if traffic is None else round(traffic / avg_launch_s / 1e9 / HBM_PEAK_GBS, 4),
-           "whole_detect_key_stream_frac": round(value / world * DETECT_BYTES / 1e9 / HBM_PEAK_GBS, 4),
+    rate = value / world  # messages per second per GPU
+    compulsory = DEVICE_KEY_BYTES / per_launch_msgs + IO_BYTES_PER_MSG + SCRATCH_BYTES_PER_MSG  # per message
+    step_measured = None
+    if pmc and pmc.get("messages_per_launch") and all(names[r] in pmc.get("kernels", {}) for r in DETECT_KERNEL_ROLES):
+        step_measured = sum(pmc["kernels"][names[r]]["hbm_bytes_per_launch"] for r in DETECT_KERNEL_ROLES) \
+            / pmc["messages_per_launch"] + pmc["kernels"].get("sum7_kernel", {}).get("hbm_bytes_per_launch", 0.0) \
+            / pmc["messages_per_launch"]
+    hbm = {"binding_roofline": "fp64-valu (DESIGN.md §5): the rotations share every key row through L2",
+           "compulsory_bytes_per_msg": round(compulsory),
+           "compulsory_GBps": round(compulsory * rate / 1e9, 2),
+           "compulsory_frac": round(compulsory * rate / 1e9 / HBM_PEAK_GBS, 5),
+           "measured_bytes_per_msg": None if step_measured is None else round(step_measured),
+           "measured_GBps": None if step_measured is None else round(step_measured * rate / 1e9, 2),
+           "measured_frac": None if step_measured is None else round(step_measured * rate / 1e9 / HBM_PEAK_GBS, 5),
+           "dominant_kernel_measured_GBps": None if traffic is None else round(traffic / avg_launch_s / 1e9, 1),
+           "key_stream_effective_GBps": round(key_stream, 1),
+           "whole_detect_key_stream_effective_GBps": round(rate * DETECT_BYTES / 1e9, 1),
+           "key_stream_note": "SURVEY §8(d) model: every key byte counted once per message; an effective rate, "
+                              "not HBM traffic (no fraction: it is not bounded by the HBM peak)",
+           "measured_from": None if pmc is None else pmc.get("source"),
            "peak": HBM_PEAK_GBS, "unit": "GB/s"}
     roof = None
     if comp and dom in comp.get("kernels", {}):
@@ -204,26 +234,21 @@ def rooflines(role, dom, launches, per_launch_msgs, launch_ms_total, value, worl
     return roof, hbm
 
 
-def free_port() -> int:
-    import socket
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    return port
-
-
 def main():
     args = parse()
     # --gpus N without an external launcher (WORLD_SIZE unset): start N ranks here, before anything
-    # touches the GPU; rank 0 prints the JSON line. WORLD_SIZE set and != N is an error.
+    # touches the GPU; rank 0 prints the JSON line. WORLD_SIZE set and != N is an error. The ranks'
+    # rendezvous store lives in this process on a port it keeps bound (omr_dist.host_rendezvous).
     try:
-        envs = omr_dist.launch_envs(args.gpus, os.environ, free_port())
+        envs = omr_dist.launch_envs(args.gpus, os.environ)
     except ValueError as e:
         print(f"[bench] {e}", file=sys.stderr, flush=True)
         sys.exit(2)
     if envs is not None:
-        sys.exit(omr_dist.spawn_ranks([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], envs))
+        store = omr_dist.host_rendezvous(envs)
+        rc = omr_dist.spawn_ranks([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], envs)
+        del store
+        sys.exit(rc)
     # The JSON line is the only thing on stdout: keep a handle on the real stdout and send fd 1
     # (library chatter, e.g. RCCL's version banner at communicator init) to stderr.
     json_out = os.fdopen(os.dup(1), "w")
@@ -232,16 +257,23 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    local = 0 if args.one_device else int(os.environ.get("LOCAL_RANK", "0"))
     dev = torch.device("cuda", local)
     if world > 1 or args.force_dist:
         import torch.distributed as dist
         for k, v in (("MASTER_ADDR", "127.0.0.1"), ("MASTER_PORT", "29511"), ("RANK", "0"), ("WORLD_SIZE", "1")):
             os.environ.setdefault(k, v)
-        dist.init_process_group("nccl", device_id=dev)
+        if args.one_device:
+            dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=dev)
     else:
         dist = None
+    if os.environ.get("OMR_BENCH_FAIL_RANK", "") == str(rank):  # test hook: a rank that dies (tests/)
+        print(f"[bench] rank {rank} failing on request (OMR_BENCH_FAIL_RANK)", file=sys.stderr, flush=True)
+        sys.exit(3)
+    torch.cuda.set_device(local)
     strong = args.total_messages is not None
     if strong:
         first, D, total = omr_dist.plan(rank, world, total=args.total_messages)
@@ -305,7 +337,7 @@ def main():
     gpu_ms = start.elapsed_time(end)
     elapsed = max(wall, gpu_ms / 1e3)
     if dist:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        tt = omr_dist._on_backend(torch.tensor([elapsed], dtype=torch.float64, device=dev), dist)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
 
@@ -327,20 +359,31 @@ def main():
 
     # Exactness certificate of the FFT external products on this run's clues: one
     # untimed pass through the guarded kernels records the largest |y - rint(y)| of every rounded
-    # coefficient; with the key's a priori bound E the run is exact when margin < 1 - E.
+    # coefficient; with the key's a priori bound E the run is exact when margin < 1 - E. The pass runs
+    # in slices of at most one launch (--batch), each compared with the timed output: the extra
+    # device memory is one slice whatever D is.
     det.rounding_margin(reset=True)
     det.set_rounding_guard(True)
-    d_guard = backend.detect(d_ca, d_cb)
+    G = min(D, args.batch)
+    g_out = torch.empty((G, 2, 2048), dtype=torch.int64, device=dev)
+    identical = True
+    for s0 in range(0, D, G):
+        n = min(G, D - s0)
+        det.detect_batch_device(d_ca[s0:].data_ptr(), d_cb[s0:].data_ptr(), n, g_out.data_ptr(), stream.cuda_stream)
+        identical &= bool(torch.equal(g_out[:n], d_out[s0:s0 + n]))
     det.set_rounding_guard(False)
     backend.synchronize()
+    del g_out
     rm = det.rounding_margin(reset=True)
+    ex = det.exactness()
     exactness = {"observed_margin": [float(f"{v:.4g}") for v in rm["observed"]],
                  "apriori_bound": [round(v, 4) for v in rm["apriori"]],
                  "certified": all(o < 1 - e for o, e in zip(rm["observed"], rm["apriori"])),
-                 "guarded_output_identical": bool(torch.equal(d_guard, d_out)),
+                 "guarded_output_identical": identical,
+                 "guarded_every_launch": ex["guarded"], "breaches": ex["breaches"],
                  "note": "level 1, level 2: largest |y - rint(y)| over every rounded FFT product coefficient "
-                         "of one untimed guarded pass; exact when observed < 1 - apriori (DESIGN.md §3a)"}
-    del d_guard
+                         "of one untimed guarded pass; exact when observed < 1 - apriori (DESIGN.md §3a); a "
+                         "level with apriori >= 0.5 would be guarded on every launch (omr_ctx_exactness)"}
 
     # correctness spot check on this rank's data: the client decrypts (library Retriever, CPU)
     # and every pertinency ciphertext must decode to [1, 0, ..., 0] or all zeros (omd.rs:48-58)
@@ -404,7 +447,7 @@ def main():
            "br2": stage["second_level_ms"] + stage["trace_ms"]}
     role = max(kms, key=kms.get)
     chunks = -(-D // args.batch)
-    roof, hbm = rooflines(role, names[role], args.steps * chunks, D / chunks, kms[role], value, world)
+    roof, hbm = rooflines(role, names[role], args.steps * chunks, D / chunks, kms[role], value, world, names)
     line = {
         "metric": "detect-phase messages/sec + per-message latency, D=65536 at 1/2/4/8 MI355X",
         "value": round(value, 2),

@@ -167,3 +167,37 @@ def test_two_rank_digest_equals_one_rank(tmp_path):
     solved = R.decode_payloads(s2, d2["pay"], w, TOTAL, sorted(found), rp.combination_count)
     for i, p in zip(sorted(found), solved):
         assert p == pay[i].tolist()
+
+
+def test_host_rendezvous_gloo_ranks(tmp_path):
+    """bench.py's launcher path: the parent hosts the TCPStore on a port it keeps bound and the
+    ranks (env:// rendezvous as agent-store clients) form a gloo group and all-reduce."""
+    import sys
+    script = tmp_path / "rank.py"
+    script.write_text(
+        "import os, sys, torch, torch.distributed as dist\n"
+        "dist.init_process_group('gloo')\n"
+        "t = torch.tensor([float(dist.get_rank() + 1)])\n"
+        "dist.all_reduce(t)\n"
+        "open(os.path.join(sys.argv[1], 'sum' + os.environ['RANK']), 'w').write(str(int(t.item())))\n"
+        "dist.destroy_process_group()\n")
+    envs = omr_dist.launch_envs(3, dict(os.environ, WORLD_SIZE=""))
+    store = omr_dist.host_rendezvous(envs)
+    assert all(e["MASTER_PORT"] == str(store.port) and e["TORCHELASTIC_USE_AGENT_STORE"] == "True" for e in envs)
+    assert omr_dist.spawn_ranks([sys.executable, str(script), str(tmp_path)], envs, poll_s=0.05) == 0
+    del store
+    assert [(tmp_path / f"sum{r}").read_text() for r in range(3)] == ["6", "6", "6"]
+
+
+def test_bench_rank_failure_propagates():
+    """bench.py --gpus 2 --one-device (the one-GPU rehearsal of the N > 1 path): a rank that dies
+    after the rendezvous makes the launcher exit non-zero (here on CPU; the full path runs on the
+    GPU in tests/test_gpu_sharded.py)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, OMR_BENCH_FAIL_RANK="1")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--one-device",
+                        "--messages", "64"], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0 and "rank 1 failing on request" in r.stderr and r.stdout == "", r.stderr[-2000:]

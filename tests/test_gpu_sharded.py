@@ -273,3 +273,42 @@ def test_detect_time_info_split():
     assert abs(t2["total_ms"] - t2["first_level_ms"] - t2["second_level_ms"] - t2["trace_ms"]) < 1e-3 * t2["total_ms"] + 1e-3
     assert t1["trace_separate"] == 0 and t1["trace_ms"] < 0.05 * t1["second_level_ms"]
     assert abs(t1["total_ms"] - t1["first_level_ms"] - t1["second_level_ms"] - t1["trace_ms"]) < 1e-3 * t1["total_ms"] + 1e-3
+
+
+def _run_bench(args, env_extra=None, timeout=420):
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, **(env_extra or {}))
+    env.pop("WORLD_SIZE", None)
+    return subprocess.run([sys.executable, "-u", os.path.join(root, "bench.py")] + args, env=env,
+                          capture_output=True, text=True, timeout=timeout)
+
+
+def test_bench_two_ranks_one_device_rehearsal():
+    """bench.py's own N > 1 path before the driver's 8-GPU run: --gpus 2
+    through the real spawn path (the launcher hosts the rendezvous store), both ranks on cuda:0
+    under a gloo group (--one-device; RCCL cannot run two ranks on one GPU): the barrier + MAX
+    all-reduce timing, the digest reduce, rank 0's single JSON line, rank 1's early return."""
+    import json
+    r = _run_bench(["--gpus", "2", "--one-device", "--messages", "2048", "--steps", "1", "--warmup", "0",
+                    "--batch", "2048"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
+    print("\n" + lines[0][:600])
+    assert line["n_gpus"] == 2 and line["config"]["messages_total"] == 4096
+    assert line["config"]["messages_per_gpu"] == 2048 and line["config"]["parallelism"] == "dp2"
+    assert line["e2e"]["ok"] and line["e2e"]["pertinent_recovered"] == 50
+    assert line["correct"] and line["exactness"]["certified"] and line["exactness"]["guarded_output_identical"]
+    assert "cpu_baseline" not in line  # rank 0 of a 2-rank job reports no CPU leg
+    assert all(not k.endswith("_frac") or v is None or v <= 1 for k, v in line["hbm"].items())
+
+
+def test_bench_two_ranks_one_device_child_failure():
+    """A rank that dies makes bench.py --gpus 2 exit non-zero with no result line."""
+    r = _run_bench(["--gpus", "2", "--one-device", "--messages", "256", "--steps", "1", "--warmup", "0"],
+                   env_extra={"OMR_BENCH_FAIL_RANK": "1"}, timeout=300)
+    assert r.returncode == 3, (r.returncode, r.stderr[-2000:])
+    assert r.stdout.strip() == ""

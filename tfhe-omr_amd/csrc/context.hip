@@ -12,6 +12,7 @@
 #include <condition_variable>
 #include <cstring>
 #include <mutex>
+#include <new>
 #include <string>
 #include <vector>
 
@@ -1126,20 +1127,33 @@ extern "C" omr_status omr_detect(omr_ctx *c, const uint16_t *ca, const uint16_t 
     std::vector<omr_ctx::DetectReq *> batch(c->queue.begin(), c->queue.begin() + (long)n);
     c->queue.erase(c->queue.begin(), c->queue.begin() + (long)n);
     lk.unlock();
-    std::vector<uint16_t> ga(n * N0), gb(n * CLUES);
-    std::vector<uint64_t> go(n * 2 * N2);
-    for (size_t k = 0; k < n; ++k) {
-      memcpy(&ga[k * N0], batch[k]->a, N0 * sizeof(uint16_t));
-      memcpy(&gb[k * CLUES], batch[k]->b, CLUES * sizeof(uint16_t));
-    }
+    // gather, launch, scatter: nothing may throw out of this extern "C" function, and the leader
+    // flag must be cleared whatever happens (a staging allocation of up to coalesce_max messages
+    // can fail): a failure becomes the batch's status
     omr_status st;
-    {
-      std::lock_guard<std::mutex> dl(c->mu);
-      st = detect_host_locked(c, ga.data(), gb.data(), n, go.data());
+    std::string err;
+    try {
+      std::vector<uint16_t> ga(n * N0), gb(n * CLUES);
+      std::vector<uint64_t> go(n * 2 * N2);
+      for (size_t k = 0; k < n; ++k) {
+        memcpy(&ga[k * N0], batch[k]->a, N0 * sizeof(uint16_t));
+        memcpy(&gb[k * CLUES], batch[k]->b, CLUES * sizeof(uint16_t));
+      }
+      {
+        std::lock_guard<std::mutex> dl(c->mu);
+        st = detect_host_locked(c, ga.data(), gb.data(), n, go.data());
+      }
+      if (st == OMR_OK)
+        for (size_t k = 0; k < n; ++k) memcpy(batch[k]->out, &go[k * 2 * N2], 2 * N2 * sizeof(uint64_t));
+      else
+        err = omr_last_error();
+    } catch (const std::bad_alloc &) {
+      st = OMR_ERR_OUT_OF_MEMORY;
+      err = "omr_detect: host staging of the coalesced batch failed";
+    } catch (...) {
+      st = OMR_ERR_DEVICE;
+      err = "omr_detect: unexpected failure while running the coalesced batch";
     }
-    const std::string err = st == OMR_OK ? std::string() : std::string(omr_last_error());
-    for (size_t k = 0; k < n; ++k)
-      if (st == OMR_OK) memcpy(batch[k]->out, &go[k * 2 * N2], 2 * N2 * sizeof(uint64_t));
     lk.lock();
     for (auto *q : batch) {
       q->st = st;

@@ -26,7 +26,7 @@ import numpy as np
 Q2 = 1125899906826241
 
 
-def launch_envs(gpus: int, environ, port: int, addr: str = "127.0.0.1"):
+def launch_envs(gpus: int, environ, port: int = 0, addr: str = "127.0.0.1"):
     """Per-rank environments for a one-process-per-GPU run of `gpus` ranks, or None when this
     process is already a rank (WORLD_SIZE set, e.g. by torch.distributed.run) or gpus == 1.
     The reference sweeps worker counts inside one program (omr_time_analyze.rs:62-101); here
@@ -49,6 +49,19 @@ def launch_envs(gpus: int, environ, port: int, addr: str = "127.0.0.1"):
                  MASTER_ADDR=addr, MASTER_PORT=str(port))
         envs.append(e)
     return envs
+
+
+def host_rendezvous(envs, addr: str = "127.0.0.1"):
+    """Host the ranks' TCPStore in this launching process, on a port the OS picks and that stays
+    bound for the whole run (a port probed and released before the ranks start could be taken by
+    another process in between), and make every rank a client of it
+    (TORCHELASTIC_USE_AGENT_STORE, the mechanism torch.distributed.run itself uses). Imports
+    torch but touches no GPU. Returns the store: keep it alive until the ranks have exited."""
+    from torch.distributed import TCPStore
+    store = TCPStore(addr, 0, len(envs), True, wait_for_workers=False)
+    for e in envs:
+        e.update(MASTER_ADDR=addr, MASTER_PORT=str(store.port), TORCHELASTIC_USE_AGENT_STORE="True")
+    return store
 
 
 def spawn_ranks(argv, envs, poll_s: float = 0.5) -> int:

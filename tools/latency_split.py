@@ -37,10 +37,8 @@ for D in [int(x) for x in sys.argv[1:]] or [1, 2, 7, 64]:
           f"ks {info['key_switch_ms']:.3f}  br2 {info['second_level_ms']:.2f}  trace {info['trace_ms']:.3f}  "
           f"device total {info['total_ms']:.2f}", flush=True)
 det.close()
-# The cooperative latency launches leave a queue that the HIP runtime tears down at exit; under
-# rocprofv3 that teardown runs after the profiler tool has finalised and faults inside
-# libhsa-runtime64 (profiles/r04/exit_fault_*). Releasing the device here, while the
-# tool is still active, leaves nothing for the exit-time teardown (OMR_KEEP_DEVICE=1 skips it).
-if os.environ.get("OMR_KEEP_DEVICE") != "1":
-    import ctypes
-    ctypes.CDLL("libamdhip64.so.7").hipDeviceReset()
+# A process that made cooperative launches (the latency path's two-CU / five-CU kernels) faults at
+# exit under rocprofv3 inside libhsa-runtime64's teardown (tools/coop_min.hip is the
+# minimal reproducer). hipDeviceReset() before exit was measured not to avoid it
+# (profiles/r04/exit_fault_probes.log), so none is made here; a profiled run that must exit cleanly
+# sets OMR_COOPERATIVE=0.
