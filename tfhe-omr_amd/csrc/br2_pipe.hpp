@@ -30,6 +30,12 @@
 
 namespace omr {
 
+#ifndef OMR_BR2Q_KB_AHEAD
+#define OMR_BR2Q_KB_AHEAD 0
+#endif
+#ifndef OMR_BR2P_SERIAL
+#define OMR_BR2P_SERIAL 0  // 1: no overlap of the two transforms (B's first half after A's MAC)
+#endif
 #ifndef OMR_BR2P_KB_EARLY
 #define OMR_BR2P_KB_EARLY 0  // output B's key blocks at the slot start (37 VGPR spills) or mid-slot
 #endif
@@ -140,10 +146,12 @@ __device__ __forceinline__ void br2p_slot(int s, int q0, const uint32_t (&pk)[2]
 #if OMR_BR2P_KB_EARLY
   br2f_load_half(kb, rsrc, br2p_row(q0, s), 1, t16);  // A's output-B key blocks, in flight all slot
 #endif
+#if !OMR_BR2P_SERIAL
   if constexpr (HAS_B) {
     const int g = s + 1, r = g >= D2 ? g - D2 : g;
     P::first_half<WB>(pk, r >> 1, br, bi, tws, t);
   }
+#endif
   F::fwd_pass<2>(ar, ai, tws, t);
   F::perm(ar, ai);
   F::fwd_pass<3>(ar, ai, tws, t);
@@ -159,6 +167,10 @@ __device__ __forceinline__ void br2p_slot(int s, int q0, const uint32_t (&pk)[2]
   br2f_load_half(ka, rsrc, br2p_row(q0, s + 1 < 2 * D2 ? s + 1 : s), 0, t16);  // next transform's output A
   P::mac<FIRST>(ar, ai, kb, sr[1], si[1]);
   if constexpr (HAS_B) {
+#if OMR_BR2P_SERIAL
+    const int g = s + 1, r = g >= D2 ? g - D2 : g;
+    P::first_half<WB>(pk, r >> 1, br, bi, tws, t);
+#endif
     P::put<1, 0>(br, bi, XB, t);
     wg_barrier_lds();
   }
@@ -316,6 +328,154 @@ __device__ __forceinline__ void br2p_body(const uint32_t *__restrict__ lwe_int, 
   }
   __syncthreads();
   hom_trace_store(acc0, acc1, xch, tw, xch + 2 * NN, tk, tb, o, t);
+}
+
+// One digit of br2q with output B's key blocks also loaded one digit ahead (OMR_BR2Q_KB_AHEAD):
+// the 32 VGPRs the LDS-resident accumulator frees hold them across the transform.
+template <int W>
+__device__ __forceinline__ void br2q_digit(const uint32_t (&pk)[2][Fft1024::E][Digits2S::DW], int j, int nx,
+                                           double (&sr)[2][2][Fft1024::E], double (&si)[2][2][Fft1024::E],
+                                           double2 (&ka)[2][Fft1024::E], double2 (&kb)[2][Fft1024::E], double2 *X,
+                                           const double2 *tws, __amdgpu_buffer_rsrc_t rsrc, uint32_t t16, int t) {
+  using F = Fft1024;
+  constexpr int E = F::E;
+  double xr[E], xi[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    xr[e] = Digits2S::digit<W>(pk[0][e], j);
+    xi[e] = Digits2S::digit<W>(pk[1][e], j);
+  }
+  F::fwd(xr, xi, X, X, tws, t);
+  Br2Pipe::mac<false>(xr, xi, ka, sr[0], si[0]);
+  br2f_load_half(ka, rsrc, nx, 0, t16);
+  Br2Pipe::mac<false>(xr, xi, kb, sr[1], si[1]);
+  br2f_load_half(kb, rsrc, nx, 1, t16);
+}
+
+// br2q: br2f_kernel's schedule (one transform at a time) with two of br2p's changes only: the
+// accumulator resident in LDS (no staging exchange, 32 VGPRs free) and the wave-local exchanges in
+// the wave's own quarter of the cross-wave buffer (no W). The cross-wave uses then alternate
+// X0, X1 over the 12 digits (issue order) and the four inverses without the staging uses between.
+template <bool G>
+__device__ __forceinline__ void br2q_body(const uint32_t *__restrict__ lwe_int, const double2 *__restrict__ bskf,
+                                          const double2 *__restrict__ twg, const double *__restrict__ tk,
+                                          DeviceTables tb, uint64_t *__restrict__ out, int mode,
+                                          unsigned long long *margin) {
+  using F = Fft1024;
+  using M = Mod<2>;
+  constexpr int E = F::E, NN = N2;
+  __shared__ double2 tws[F::n];
+  __shared__ double2 lds[4][F::n];  // X0, X1, ACC (mask, body); the trace's 3 N2 doubles afterwards
+  double2(&Xb)[2][F::n] = *reinterpret_cast<double2(*)[2][F::n]>(&lds[0][0]);
+  double *acs = reinterpret_cast<double *>(&lds[2][0]);
+  const int t = threadIdx.x;
+  const uint32_t *lwe = lwe_int + (size_t)blockIdx.x * (NI + 1);
+  F::load_twiddles(tws, twg, t);
+  {
+    const int b = (int)lwe[NI];
+    const int rr = (2 * NN - (b % (2 * NN))) % (2 * NN);
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const int c = F::idx(0, t, e) + F::n * h;
+        acs[F::slot_stage(c)] = 0.0;
+        acs[NN + F::slot_stage(c)] = canon_small<M>(rot_read<NN>(tb.lut2, c, rr));
+      }
+  }
+  double2 ka[2][E], kb[2][E];
+  const __amdgpu_buffer_rsrc_t rsrc = bsk2_rsrc(bskf);
+  const uint32_t t16 = (uint32_t)t * 16u;
+  RoundGuard<G> rg;
+#pragma unroll 1
+  for (int i = 0; i < NI; ++i) {
+    const int a = (int)__builtin_amdgcn_readfirstlane(lwe[i]) & (2 * NN - 1);
+    if (a == 0) continue;
+    const int q0 = i * 2 * D2;
+    br2f_load_half(ka, rsrc, q0, 0, t16);
+#if OMR_BR2Q_KB_AHEAD
+    br2f_load_half(kb, rsrc, q0, 1, t16);
+#endif
+    wg_barrier_lds();  // ACC visible; the previous step's last inverse reads done
+    double sr[2][2][E], si[2][2][E];
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      uint32_t pk[2][E][Digits2S::DW];
+      Br2Pipe::digits(acs + p * NN, a, t, pk);
+      auto nxt = [&](int j, int w) {
+        return q0 + (w == 0 ? p * D2 + j + 3 : (j + 1 < D2 / 2 ? p * D2 + j + 1 : (p == 0 ? D2 : 2 * D2 - 1)));
+      };
+      if (p == 0) {
+#pragma unroll
+        for (int o = 0; o < 2; ++o)
+#pragma unroll
+          for (int l = 0; l < 2; ++l)
+#pragma unroll
+            for (int e = 0; e < E; ++e) sr[o][l][e] = si[o][l][e] = 0.0;
+      }
+#pragma unroll 1
+      for (int j = 0; j < D2 / 2; ++j) {
+#if OMR_BR2Q_KB_AHEAD
+        br2q_digit<0>(pk, j, nxt(j, 0), sr, si, ka, kb, Xb[0], tws, rsrc, t16, t);
+        br2q_digit<1>(pk, j, nxt(j, 1), sr, si, ka, kb, Xb[1], tws, rsrc, t16, t);
+#else
+        br2f_digit<0>(pk, j, q0 + p * D2 + j, nxt(j, 0), sr, si, ka, kb, Xb[0], Xb[0], tws, rsrc, t16, t);
+        br2f_digit<1>(pk, j, q0 + p * D2 + j + 3, nxt(j, 1), sr, si, ka, kb, Xb[1], Xb[1], tws, rsrc, t16, t);
+#endif
+      }
+    }
+#pragma unroll
+    for (int o = 0; o < 2; ++o) {
+#pragma unroll
+      for (int l = 0; l < 2; ++l) F::inv(sr[o][l], si[o][l], Xb[l], Xb[l], tws, t);
+      br2p_update<G>(acs + o * NN, sr[o], si[o], rg, t);
+    }
+  }
+  rg.publish(margin);
+  __syncthreads();
+  uint64_t *o = out + (size_t)blockIdx.x * 2 * NN;
+  if (mode == 1) {
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const int c = F::idx(0, t, e) + F::n * h;
+          o[p * NN + c] = to_u64<M>(acs[p * NN + F::slot_stage(c)]);
+        }
+    return;
+  }
+  double acc0[BR2_E], acc1[BR2_E];
+#pragma unroll
+  for (int e = 0; e < BR2_E; ++e) {
+    acc0[e] = acs[F::slot_stage(t + e * BR2_T)];
+    acc1[e] = acs[NN + F::slot_stage(t + e * BR2_T)];
+  }
+  double *xch = reinterpret_cast<double *>(&lds[0][0]);
+  double *tw = reinterpret_cast<double *>(tws);
+  __syncthreads();
+#pragma unroll
+  for (int e = 0; e < BR2_E; ++e) {
+    tw[t + e * BR2_T] = tb.tw2[t + e * BR2_T];
+    xch[2 * NN + t + e * BR2_T] = tb.itw2[t + e * BR2_T];
+  }
+  __syncthreads();
+  hom_trace_store(acc0, acc1, xch, tw, xch + 2 * NN, tk, tb, o, t);
+}
+
+__global__ __launch_bounds__(256, 2) void br2q_kernel(const uint32_t *__restrict__ lwe_int,
+                                                      const double2 *__restrict__ bskf,
+                                                      const double2 *__restrict__ twg, const double *__restrict__ tk,
+                                                      DeviceTables tb, uint64_t *__restrict__ out, int mode) {
+  br2q_body<false>(lwe_int, bskf, twg, tk, tb, out, mode, nullptr);
+}
+__global__ __launch_bounds__(256, 2) void br2q_guard_kernel(const uint32_t *__restrict__ lwe_int,
+                                                            const double2 *__restrict__ bskf,
+                                                            const double2 *__restrict__ twg, const double *__restrict__ tk,
+                                                            DeviceTables tb, uint64_t *__restrict__ out, int mode,
+                                                            unsigned long long *margin) {
+  br2q_body<true>(lwe_int, bskf, twg, tk, tb, out, mode, margin);
 }
 
 __global__ __launch_bounds__(256, 2) void br2p_kernel(const uint32_t *__restrict__ lwe_int,

@@ -333,7 +333,11 @@ struct omr_ctx {
 #ifndef OMR_BR2_PIPE
 #define OMR_BR2_PIPE 0
 #endif
-#if OMR_BR2_PIPE
+#if OMR_BR2_PIPE == 2
+#define OMR_BR2_NAME "br2q_kernel"
+#define OMR_BR2_KERNEL br2q_kernel
+#define OMR_BR2_GUARD_KERNEL br2q_guard_kernel
+#elif OMR_BR2_PIPE
 #define OMR_BR2_NAME "br2p_kernel"
 #define OMR_BR2_KERNEL br2p_kernel
 #define OMR_BR2_GUARD_KERNEL br2p_guard_kernel
