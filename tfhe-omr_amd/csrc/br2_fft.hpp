@@ -216,6 +216,52 @@ struct Fft1024 {
     __builtin_amdgcn_wave_barrier();  // the next writes stay below these reads (in-order LDS per wave)
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
   }
+  // passes with the block's twiddles (B, A, AB) already in registers
+  __device__ static __forceinline__ void fwd_pass_r(double (&xr)[E], double (&xi)[E], const double2 (&w)[3]) {
+    cmul(xr[1], xi[1], w[0].x, w[0].y);
+    cmul(xr[2], xi[2], w[1].x, w[1].y);
+    cmul(xr[3], xi[3], w[2].x, w[2].y);
+    net4(xr, xi);
+  }
+  __device__ static __forceinline__ void inv_pass_r(double (&xr)[E], double (&xi)[E], const double2 (&w)[3]) {
+    inet4(xr, xi);
+    cmulc(xr[1], xi[1], w[0].x, w[0].y);
+    cmulc(xr[2], xi[2], w[1].x, w[1].y);
+    cmulc(xr[3], xi[3], w[2].x, w[2].y);
+  }
+  template <int P>
+  __device__ static __forceinline__ void block_twiddles(double2 (&w)[3], const double2 *tws, int t) {
+    const int b = block<P>(t);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) w[k] = tws[tw_slot(P, b, k)];
+  }
+  // fwd / inv with passes 3 and 4 on register twiddles (w3, w4: block_twiddles<3>, <4> of this thread)
+  __device__ static __forceinline__ void fwd_r(double (&xr)[E], double (&xi)[E], double2 *X, double2 *W,
+                                               const double2 *tws, int t, const double2 (&w3)[3],
+                                               const double2 (&w4)[3]) {
+    fwd_pass<0>(xr, xi, tws, t);
+    perm(xr, xi);
+    fwd_pass<1>(xr, xi, tws, t);
+    exchange<1, 2, 0, true>(xr, xi, X, t);
+    fwd_pass<2>(xr, xi, tws, t);
+    perm(xr, xi);
+    fwd_pass_r(xr, xi, w3);
+    exchange<3, 4, 2, false>(xr, xi, W, t);
+    fwd_pass_r(xr, xi, w4);
+  }
+  __device__ static __forceinline__ void inv_r(double (&xr)[E], double (&xi)[E], double2 *X, double2 *W,
+                                               const double2 *tws, int t, const double2 (&w3)[3],
+                                               const double2 (&w4)[3]) {
+    inv_pass_r(xr, xi, w4);
+    exchange<4, 3, 3, false>(xr, xi, W, t);
+    inv_pass_r(xr, xi, w3);
+    perm(xr, xi);
+    inv_pass<2>(xr, xi, tws, t);
+    exchange<2, 1, 1, true>(xr, xi, X, t);
+    inv_pass<1>(xr, xi, tws, t);
+    perm(xr, xi);
+    inv_pass<0>(xr, xi, tws, t);
+  }
   // forward: in P0 layout (point idx(0, t, e)), out P4 layout; X: this transform's cross-wave
   // buffer, W: the wave-local buffer
   __device__ static __forceinline__ void fwd(double (&xr)[E], double (&xi)[E], double2 *X, double2 *W,

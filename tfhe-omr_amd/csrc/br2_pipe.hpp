@@ -30,6 +30,9 @@
 
 namespace omr {
 
+#ifndef OMR_BR2Q_TWR
+#define OMR_BR2Q_TWR 0  // br2q: passes 3 and 4 on twiddles held in registers
+#endif
 #ifndef OMR_BR2Q_KB_AHEAD
 #define OMR_BR2Q_KB_AHEAD 0
 #endif
@@ -333,10 +336,11 @@ __device__ __forceinline__ void br2p_body(const uint32_t *__restrict__ lwe_int, 
 // One digit of br2q with output B's key blocks also loaded one digit ahead (OMR_BR2Q_KB_AHEAD):
 // the 32 VGPRs the LDS-resident accumulator frees hold them across the transform.
 template <int W>
-__device__ __forceinline__ void br2q_digit(const uint32_t (&pk)[2][Fft1024::E][Digits2S::DW], int j, int nx,
+__device__ __forceinline__ void br2q_digit(const uint32_t (&pk)[2][Fft1024::E][Digits2S::DW], int j, int q, int nx,
                                            double (&sr)[2][2][Fft1024::E], double (&si)[2][2][Fft1024::E],
                                            double2 (&ka)[2][Fft1024::E], double2 (&kb)[2][Fft1024::E], double2 *X,
-                                           const double2 *tws, __amdgpu_buffer_rsrc_t rsrc, uint32_t t16, int t) {
+                                           const double2 *tws, __amdgpu_buffer_rsrc_t rsrc, uint32_t t16, int t,
+                                           const double2 (&w3)[3], const double2 (&w4)[3]) {
   using F = Fft1024;
   constexpr int E = F::E;
   double xr[E], xi[E];
@@ -345,11 +349,22 @@ __device__ __forceinline__ void br2q_digit(const uint32_t (&pk)[2][Fft1024::E][D
     xr[e] = Digits2S::digit<W>(pk[0][e], j);
     xi[e] = Digits2S::digit<W>(pk[1][e], j);
   }
+#if OMR_BR2Q_TWR
+  F::fwd_r(xr, xi, X, X, tws, t, w3, w4);
+#else
   F::fwd(xr, xi, X, X, tws, t);
+#endif
+#if OMR_BR2Q_KB_AHEAD
   Br2Pipe::mac<false>(xr, xi, ka, sr[0], si[0]);
   br2f_load_half(ka, rsrc, nx, 0, t16);
   Br2Pipe::mac<false>(xr, xi, kb, sr[1], si[1]);
   br2f_load_half(kb, rsrc, nx, 1, t16);
+#else
+  br2f_load_half(kb, rsrc, q, 1, t16);
+  Br2Pipe::mac<false>(xr, xi, ka, sr[0], si[0]);
+  br2f_load_half(ka, rsrc, nx, 0, t16);
+  Br2Pipe::mac<false>(xr, xi, kb, sr[1], si[1]);
+#endif
 }
 
 // br2q: br2f_kernel's schedule (one transform at a time) with two of br2p's changes only: the
@@ -386,6 +401,12 @@ __device__ __forceinline__ void br2q_body(const uint32_t *__restrict__ lwe_int, 
   double2 ka[2][E], kb[2][E];
   const __amdgpu_buffer_rsrc_t rsrc = bsk2_rsrc(bskf);
   const uint32_t t16 = (uint32_t)t * 16u;
+  double2 w3[3], w4[3];  // this thread's pass-3 / pass-4 block twiddles (OMR_BR2Q_TWR)
+#if OMR_BR2Q_TWR
+  __syncthreads();
+  F::block_twiddles<3>(w3, tws, t);
+  F::block_twiddles<4>(w4, tws, t);
+#endif
   RoundGuard<G> rg;
 #pragma unroll 1
   for (int i = 0; i < NI; ++i) {
@@ -415,19 +436,20 @@ __device__ __forceinline__ void br2q_body(const uint32_t *__restrict__ lwe_int, 
       }
 #pragma unroll 1
       for (int j = 0; j < D2 / 2; ++j) {
-#if OMR_BR2Q_KB_AHEAD
-        br2q_digit<0>(pk, j, nxt(j, 0), sr, si, ka, kb, Xb[0], tws, rsrc, t16, t);
-        br2q_digit<1>(pk, j, nxt(j, 1), sr, si, ka, kb, Xb[1], tws, rsrc, t16, t);
-#else
-        br2f_digit<0>(pk, j, q0 + p * D2 + j, nxt(j, 0), sr, si, ka, kb, Xb[0], Xb[0], tws, rsrc, t16, t);
-        br2f_digit<1>(pk, j, q0 + p * D2 + j + 3, nxt(j, 1), sr, si, ka, kb, Xb[1], Xb[1], tws, rsrc, t16, t);
-#endif
+        br2q_digit<0>(pk, j, q0 + p * D2 + j, nxt(j, 0), sr, si, ka, kb, Xb[0], tws, rsrc, t16, t, w3, w4);
+        br2q_digit<1>(pk, j, q0 + p * D2 + j + 3, nxt(j, 1), sr, si, ka, kb, Xb[1], tws, rsrc, t16, t, w3, w4);
       }
     }
 #pragma unroll
     for (int o = 0; o < 2; ++o) {
 #pragma unroll
-      for (int l = 0; l < 2; ++l) F::inv(sr[o][l], si[o][l], Xb[l], Xb[l], tws, t);
+      for (int l = 0; l < 2; ++l) {
+#if OMR_BR2Q_TWR
+        F::inv_r(sr[o][l], si[o][l], Xb[l], Xb[l], tws, t, w3, w4);
+#else
+        F::inv(sr[o][l], si[o][l], Xb[l], Xb[l], tws, t);
+#endif
+      }
       br2p_update<G>(acs + o * NN, sr[o], si[o], rg, t);
     }
   }
