@@ -96,3 +96,24 @@ def test_product_exact_random_and_adversarial():
         err = np.max(np.abs(got - want.astype(np.float64)))
         assert abs(float(want[c])) > 2**44 and err < 0.1, (c, err)
         assert np.array_equal(np.rint(got).astype(np.int64).astype(object), want)
+
+
+def test_exchange_regions():
+    """br2f_kernel runs each wave-local exchange in the wave's own quarter of the transform's
+    cross-wave buffer X (no separate W buffer, round 5). Safe because every exchange direction puts
+    wave w's points at slots whose bits 9, 8 equal w on its own side: the forward cross-wave reads
+    (P2, xf) and the inverse cross-wave writes (P2, xi) are own-quarter, and both wave-local
+    exchanges (wf, wi) are own-quarter on both sides. So after a forward transform's cross-wave reads
+    no other wave touches quarter w of X until the next-but-one transform writes X behind the next
+    barrier, and an inverse's wave-local exchange precedes its own-quarter cross-wave writes."""
+    import fft2_model as M
+    own = {"xf": ("read",), "xi": ("write",), "wf": ("write", "read"), "wi": ("write", "read")}
+    for name, sides in own.items():
+        sw, (pf, pt) = M.SWIZZLES[name], M.EXCHANGES[name]
+        for side in sides:
+            p = pf if side == "write" else pt
+            assert all((sw(M.idx(p, t, e)) >> 8) == (t >> 6) for t in range(M.T) for e in range(M.E)), (name, side)
+    # the other side of a cross-wave exchange spans every quarter (it is cross-wave)
+    for name, side, p in (("xf", "write", 1), ("xi", "read", 1)):
+        sw = M.SWIZZLES[name]
+        assert {sw(M.idx(p, t, e)) >> 8 for t in range(64) for e in range(M.E)} == {0, 1, 2, 3}, (name, side)

@@ -229,16 +229,20 @@ struct Fft1024 {
     cmulc(xr[2], xi[2], w[1].x, w[1].y);
     cmulc(xr[3], xi[3], w[2].x, w[2].y);
   }
+  // thread t's twiddles of pass P (its block is the same for all four registers and all transforms)
   template <int P>
   __device__ static __forceinline__ void block_twiddles(double2 (&w)[3], const double2 *tws, int t) {
     const int b = block<P>(t);
 #pragma unroll
     for (int k = 0; k < 3; ++k) w[k] = tws[tw_slot(P, b, k)];
   }
-  // fwd / inv with passes 3 and 4 on register twiddles (w3, w4: block_twiddles<3>, <4> of this thread)
-  __device__ static __forceinline__ void fwd_r(double (&xr)[E], double (&xi)[E], double2 *X, double2 *W,
-                                               const double2 *tws, int t, const double2 (&w3)[3],
-                                               const double2 (&w4)[3]) {
+  // forward: in P0 layout (point idx(0, t, e)), out P4 layout. X: this transform's cross-wave buffer;
+  // the wave-local exchange (P3 -> P4) runs in the wave's own quarter of X (slot bits 9, 8 = wave:
+  // tests/test_fft2_layout.py::test_exchange_regions), which after this transform's cross-wave reads
+  // no other wave touches until the next-but-one transform writes X behind the next barrier. Passes
+  // 3 and 4 on the thread's twiddles held in registers (w3, w4: block_twiddles<3>, <4>).
+  __device__ static __forceinline__ void fwd(double (&xr)[E], double (&xi)[E], double2 *X, const double2 *tws, int t,
+                                             const double2 (&w3)[3], const double2 (&w4)[3]) {
     fwd_pass<0>(xr, xi, tws, t);
     perm(xr, xi);
     fwd_pass<1>(xr, xi, tws, t);
@@ -246,42 +250,18 @@ struct Fft1024 {
     fwd_pass<2>(xr, xi, tws, t);
     perm(xr, xi);
     fwd_pass_r(xr, xi, w3);
-    exchange<3, 4, 2, false>(xr, xi, W, t);
+    exchange<3, 4, 2, false>(xr, xi, X, t);
     fwd_pass_r(xr, xi, w4);
   }
-  __device__ static __forceinline__ void inv_r(double (&xr)[E], double (&xi)[E], double2 *X, double2 *W,
-                                               const double2 *tws, int t, const double2 (&w3)[3],
-                                               const double2 (&w4)[3]) {
+  // unscaled inverse (x 1024; the keys carry 1/1024): in P4 layout, out P0 layout; the wave-local
+  // exchange first, in the wave's own quarter of X (which the previous use of X, two cross-wave
+  // uses back, has finished with behind the last barrier), then the cross-wave one (own-quarter
+  // writes)
+  __device__ static __forceinline__ void inv(double (&xr)[E], double (&xi)[E], double2 *X, const double2 *tws, int t,
+                                             const double2 (&w3)[3], const double2 (&w4)[3]) {
     inv_pass_r(xr, xi, w4);
-    exchange<4, 3, 3, false>(xr, xi, W, t);
+    exchange<4, 3, 3, false>(xr, xi, X, t);
     inv_pass_r(xr, xi, w3);
-    perm(xr, xi);
-    inv_pass<2>(xr, xi, tws, t);
-    exchange<2, 1, 1, true>(xr, xi, X, t);
-    inv_pass<1>(xr, xi, tws, t);
-    perm(xr, xi);
-    inv_pass<0>(xr, xi, tws, t);
-  }
-  // forward: in P0 layout (point idx(0, t, e)), out P4 layout; X: this transform's cross-wave
-  // buffer, W: the wave-local buffer
-  __device__ static __forceinline__ void fwd(double (&xr)[E], double (&xi)[E], double2 *X, double2 *W,
-                                             const double2 *tws, int t) {
-    fwd_pass<0>(xr, xi, tws, t);
-    perm(xr, xi);
-    fwd_pass<1>(xr, xi, tws, t);
-    exchange<1, 2, 0, true>(xr, xi, X, t);
-    fwd_pass<2>(xr, xi, tws, t);
-    perm(xr, xi);
-    fwd_pass<3>(xr, xi, tws, t);
-    exchange<3, 4, 2, false>(xr, xi, W, t);
-    fwd_pass<4>(xr, xi, tws, t);
-  }
-  // unscaled inverse (x 1024; the keys carry 1/1024): in P4 layout, out P0 layout
-  __device__ static __forceinline__ void inv(double (&xr)[E], double (&xi)[E], double2 *X, double2 *W,
-                                             const double2 *tws, int t) {
-    inv_pass<4>(xr, xi, tws, t);
-    exchange<4, 3, 3, false>(xr, xi, W, t);
-    inv_pass<3>(xr, xi, tws, t);
     perm(xr, xi);
     inv_pass<2>(xr, xi, tws, t);
     exchange<2, 1, 1, true>(xr, xi, X, t);
@@ -349,17 +329,41 @@ __device__ __forceinline__ void br2f_load_half(double2 (&k)[2][Fft1024::E], __am
     }
 }
 
-// One digit of a CMUX step: forward transform of digit j + 3 w of poly p (its words pk), then the
-// multiply-accumulate into the four (output, limb) spectra: output A with ka (loaded one digit
-// ahead), output B with kb (loaded after the transform); ka is reloaded for the next digit nx
-// between the two.
-// (A function, not a lambda: by-reference captures drop __restrict__ / address-space facts.)
+// Digit words of (X^a - 1) * ACC_p from the LDS-resident accumulator (acp: 2048 doubles at
+// Fft1024::slot_stage positions): coefficient j and j + 1024 of the thread's P0 points, as the
+// Digits2S words (the rotated entry with its negacyclic sign as one xor of bit 63).
+__device__ __forceinline__ void br2f_digits(const double *acp, int a, int t,
+                                            uint32_t (&pk)[2][Fft1024::E][Digits2S::DW]) {
+  using F = Fft1024;
+  using M = Mod<2>;
+  constexpr int NN = N2;
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int e = 0; e < F::E; ++e) {
+      const int c = F::idx(0, t, e) + F::n * h;
+      const uint32_t u = (uint32_t)(c - a) & (2 * NN - 1);
+      const double v = acp[F::slot_stage(u & (NN - 1))];
+      const uint32_t vh = (uint32_t)(__builtin_bit_cast(uint64_t, v) >> 32) ^ ((u & NN) << (31 - 11));
+      const double rot = __builtin_bit_cast(double, (__builtin_bit_cast(uint64_t, v) & 0xffffffffull) |
+                                                        ((uint64_t)vh << 32));
+      Digits2S::pack(canon_small<M>(rot - acp[F::slot_stage(c)]), pk[h][e]);
+      // keep the words as integers (not the doubles they come from) across the digit loop
+      asm volatile("" : "+v"(pk[h][e][0]), "+v"(pk[h][e][1]));
+    }
+}
+
+// One digit of a CMUX step: forward transform of digit j + 3 w (W) of the poly whose words are pk,
+// then the multiply-accumulate into the four (output, limb) spectra: output A with ka (loaded one
+// digit ahead, in flight across the transform), output B with kb (loaded after the transform, in
+// flight across output A's multiply-accumulate); ka is reloaded for the next digit nx between the
+// two. (A function, not a lambda: by-reference captures drop __restrict__ / address-space facts.)
 template <int W>
 __device__ __forceinline__ void br2f_digit(const uint32_t (&pk)[2][Fft1024::E][Digits2S::DW], int j, int q, int nx,
                                            double (&sr)[2][2][Fft1024::E], double (&si)[2][2][Fft1024::E],
-                                           double2 (&ka)[2][Fft1024::E], double2 (&kb)[2][Fft1024::E],
-                                           double2 *X, double2 *Wb, const double2 *tws, __amdgpu_buffer_rsrc_t rsrc,
-                                           uint32_t t16, int t) {
+                                           double2 (&ka)[2][Fft1024::E], double2 (&kb)[2][Fft1024::E], double2 *X,
+                                           const double2 *tws, __amdgpu_buffer_rsrc_t rsrc, uint32_t t16, int t,
+                                           const double2 (&w3)[3], const double2 (&w4)[3]) {
   using F = Fft1024;
   constexpr int E = F::E;
   double xr[E], xi[E];
@@ -368,7 +372,7 @@ __device__ __forceinline__ void br2f_digit(const uint32_t (&pk)[2][Fft1024::E][D
     xr[e] = Digits2S::digit<W>(pk[0][e], j);
     xi[e] = Digits2S::digit<W>(pk[1][e], j);
   }
-  F::fwd(xr, xi, X, Wb, tws, t);
+  F::fwd(xr, xi, X, tws, t, w3, w4);
   br2f_load_half(kb, rsrc, q, 1, t16);
 #pragma unroll
   for (int o = 0; o < 2; ++o) {
@@ -384,17 +388,41 @@ __device__ __forceinline__ void br2f_digit(const uint32_t (&pk)[2][Fft1024::E][D
   }
 }
 
+// Rounding to the exact limb products, recombination mod q2 and ACC_o += (in place in LDS): thread
+// t owns coefficients idx(0, t, e) + 1024 h of ACC_o, which only it reads before the next step.
+template <bool G>
+__device__ __forceinline__ void br2f_update(double *aco, const double (&sr)[2][Fft1024::E],
+                                           const double (&si)[2][Fft1024::E], RoundGuard<G> &rg, int t) {
+  using F = Fft1024;
+  using M = Mod<2>;
+#pragma unroll
+  for (int e = 0; e < F::E; ++e)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const double ylo = h ? si[0][e] : sr[0][e], yhi = h ? si[1][e] : sr[1][e];
+      const double lo = rint(ylo), hr = rint(yhi);
+      rg.note(ylo, lo);
+      rg.note(yhi, hr);
+      const double hi = hr * LIMB;  // exact (|P_hi| < 2^45)
+      double &a = aco[F::slot_stage(F::idx(0, t, e) + F::n * h)];
+      a = canon<M>(a + red<M>(hi) + lo);
+    }
+}
+
 // Level-2 blind rotation (BlindRotationKey::blind_rotate, detector.rs:623) on the exact FFT: one
-// 256-thread workgroup per message, ACC in registers (P0 layout: coefficients j and j + 1024 of the
-// thread's 4 points), output the coefficient-domain rotation u64 [2][2048] (trace_kernel follows).
-// Per CMUX step: stage ACC_p in LDS, digits of (X^a - 1) * ACC_p (the NTT kernels' Digits2), and
-// for each digit a forward transform and the multiply-accumulate into the four (output, limb)
-// spectra with the key row, which is loaded one digit ahead; then the four inverses, rounding,
-// limb recombination mod q2 and the accumulator update. Cross-wave LDS uses alternate X1, X0 in a
-// fixed order (staging mask X1, mask digits X0 X1 X0 X1 X0 X1, staging body X0, body digits X1 ..
-// X0, inverses X1 X0 X1 X0), so no use needs a trailing barrier (the rule of cmux_step3).
-// mode 0: then hom_trace (detector.rs:626-639) with the accumulator re-laid out for the trace's
-// NTTs, output the NttRlweCiphertext; mode 1: the coefficient-domain rotation (stage tests).
+// 256-thread workgroup per message; output the coefficient-domain rotation (mode 1) or, after
+// hom_trace (detector.rs:626-639), the NttRlweCiphertext (mode 0).
+// The accumulator lives in LDS (ACC_p at slot_stage positions): each step reads the rotated digits
+// of ACC_p straight from it and the update writes it in place, so there is no staging exchange and
+// its 32 VGPRs hold the thread's pass-3 / pass-4 twiddles instead (round 5). Per CMUX step: for
+// each of the 12 digits in issue order (poly p, digit j + 3 w) a forward transform and the
+// multiply-accumulate into the four (output, limb) spectra with the key row (output A's blocks
+// loaded one digit ahead); then the four inverses, rounding, limb recombination mod q2 and the
+// update. Cross-wave uses alternate X0, X1 over the 12 digits and the 4 inverses, and every
+// wave-local exchange runs in the wave's own quarter of the current X (Fft1024::fwd / inv), so each
+// use rewrites a buffer whose readers have passed a later barrier: 17 workgroup barriers per step
+// (one at the step start: the previous update visible to the rotated reads).
+// LDS: twiddles 16 KB, X0 / X1 32 KB, ACC 32 KB (80 KB: two workgroups per CU).
 template <bool G>
 __device__ __forceinline__ void br2f_body(const uint32_t *__restrict__ lwe_int, const double2 *__restrict__ bskf,
                                           const double2 *__restrict__ twg, const double *__restrict__ tk,
@@ -405,31 +433,28 @@ __device__ __forceinline__ void br2f_body(const uint32_t *__restrict__ lwe_int, 
   constexpr int E = F::E, NN = N2;
   static_assert(F::TW_LEN <= F::n, "the twiddle table's LDS doubles as the trace's NTT table");
   __shared__ double2 tws[F::n];
-  __shared__ double2 lds2[3][F::n];  // X0, X1, W; the trace's 3 N2 doubles afterwards
-  double2(&Xb)[2][F::n] = *reinterpret_cast<double2(*)[2][F::n]>(&lds2[0][0]);
-  double2 *W = lds2[2];
+  __shared__ double2 lds[4][F::n];  // X0, X1, ACC (mask, body); the trace's 3 N2 doubles afterwards
+  double2(&Xb)[2][F::n] = *reinterpret_cast<double2(*)[2][F::n]>(&lds[0][0]);
+  double *acs = reinterpret_cast<double *>(&lds[2][0]);
   const int t = threadIdx.x;
   const uint32_t *lwe = lwe_int + (size_t)blockIdx.x * (NI + 1);
   F::load_twiddles(tws, twg, t);
-  // ACC = (0, X^{-b} * LUT2): ac[p][h][e] = coefficient idx(0, t, e) + 1024 h of poly p
-  double ac[2][2][E];
-  {
+  {  // ACC = (0, X^{-b} * LUT2)
     const int b = (int)lwe[NI];
     const int rr = (2 * NN - (b % (2 * NN))) % (2 * NN);
 #pragma unroll
     for (int h = 0; h < 2; ++h)
 #pragma unroll
       for (int e = 0; e < E; ++e) {
-        ac[0][h][e] = 0.0;
-        ac[1][h][e] = canon_small<M>(rot_read<NN>(tb.lut2, F::idx(0, t, e) + F::n * h, rr));
+        const int c = F::idx(0, t, e) + F::n * h;
+        acs[F::slot_stage(c)] = 0.0;
+        acs[NN + F::slot_stage(c)] = canon_small<M>(rot_read<NN>(tb.lut2, c, rr));
       }
   }
   __syncthreads();
-  // key row: thread t's 4 points of each (output, limb) block, for the digits in issue order. The
-  // output-A blocks of the next digit are loaded one digit ahead (in flight across its transform);
-  // the output-B blocks are loaded after the transform (in flight across output A's
-  // multiply-accumulate): 32 VGPRs fewer across the transform. Loading them earlier (before or
-  // inside the transform) measured 43-50 % slower (profiles/r03/level2_experiments.log).
+  double2 w3[3], w4[3];  // this thread's pass-3 / pass-4 twiddles, for every transform of the rotation
+  F::block_twiddles<3>(w3, tws, t);
+  F::block_twiddles<4>(w4, tws, t);
   double2 ka[2][E], kb[2][E];
   const __amdgpu_buffer_rsrc_t rsrc = bsk2_rsrc(bskf);
   const uint32_t t16 = (uint32_t)t * 16u;
@@ -440,38 +465,16 @@ __device__ __forceinline__ void br2f_body(const uint32_t *__restrict__ lwe_int, 
     if (a == 0) continue;  // (X^0 - 1) * ACC = 0
     const int q0 = i * 2 * D2;  // the step's first global row
     br2f_load_half(ka, rsrc, q0, 0, t16);
+    wg_barrier_lds();  // ACC (init or the previous update) visible; the previous inverses' reads done
     double sr[2][2][E], si[2][2][E];  // [output][limb] spectra
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
       uint32_t pk[2][E][Digits2S::DW];  // [coefficient j / j + 1024][point] digit words
-      {  // digits of (X^a - 1) * ACC_p, staged in X1 (mask) / X0 (body)
-        double *st = reinterpret_cast<double *>(Xb[p == 0 ? 1 : 0]);
-#pragma unroll
-        for (int h = 0; h < 2; ++h)
-#pragma unroll
-          for (int e = 0; e < E; ++e) st[F::slot_stage(F::idx(0, t, e) + F::n * h)] = ac[p][h][e];
-        wg_barrier_lds();
-#pragma unroll
-        for (int h = 0; h < 2; ++h)
-#pragma unroll
-          for (int e = 0; e < E; ++e) {
-            const uint32_t u = (uint32_t)(F::idx(0, t, e) + F::n * h - a) & (2 * NN - 1);
-            const double v = st[F::slot_stage(u & (NN - 1))];
-            const uint32_t vh = (uint32_t)(__builtin_bit_cast(uint64_t, v) >> 32) ^ ((u & NN) << (31 - 11));
-            const double rot = __builtin_bit_cast(double, (__builtin_bit_cast(uint64_t, v) & 0xffffffffull) |
-                                                              ((uint64_t)vh << 32));
-            Digits2S::pack(canon_small<M>(rot - ac[p][h][e]), pk[h][e]);
-            // keep the words as integers (not the doubles they come from) across the digit loop
-            asm volatile("" : "+v"(pk[h][e][0]), "+v"(pk[h][e][1]));
-          }
-        __builtin_amdgcn_wave_barrier();
-        __atomic_signal_fence(__ATOMIC_SEQ_CST);
-      }
+      br2f_digits(acs + p * NN, a, t, pk);
       // digits in issue order g = 2 j + w: digit j + 3 w sits in word w at field j, so the word is
-      // chosen at compile time; its GGSW row is p D2 + j + 3 w. Cross-wave buffers: mask digits X0,
-      // X1, ..., body digits X1, X0, ... (X_{(w + p) & 1}). The next digit in issue order (the last
-      // digit reloads its own row: harmless): after (j, 0) comes (j, 1), after (j, 1) (j + 1, 0),
-      // after the mask's last digit the body's first, after the body's last itself.
+      // chosen at compile time; its GGSW row is p D2 + j + 3 w. The next digit in issue order (the
+      // last digit reloads its own row: harmless): after (j, 0) comes (j, 1), after (j, 1)
+      // (j + 1, 0), after the mask's last digit the body's first, after the body's last itself.
       auto nxt = [&](int j, int w) {
         return q0 + (w == 0 ? p * D2 + j + 3 : (j + 1 < D2 / 2 ? p * D2 + j + 1 : (p == 0 ? D2 : 2 * D2 - 1)));
       };
@@ -485,30 +488,20 @@ __device__ __forceinline__ void br2f_body(const uint32_t *__restrict__ lwe_int, 
       }
 #pragma unroll 1
       for (int j = 0; j < D2 / 2; ++j) {
-        br2f_digit<0>(pk, j, q0 + p * D2 + j, nxt(j, 0), sr, si, ka, kb, Xb[p & 1], W, tws, rsrc, t16, t);
-        br2f_digit<1>(pk, j, q0 + p * D2 + j + 3, nxt(j, 1), sr, si, ka, kb, Xb[(1 + p) & 1], W, tws, rsrc, t16,
-                      t);
+        br2f_digit<0>(pk, j, q0 + p * D2 + j, nxt(j, 0), sr, si, ka, kb, Xb[0], tws, rsrc, t16, t, w3, w4);
+        br2f_digit<1>(pk, j, q0 + p * D2 + j + 3, nxt(j, 1), sr, si, ka, kb, Xb[1], tws, rsrc, t16, t, w3, w4);
       }
     }
-    // inverses (X1, X0, X1, X0), rounding to the exact limb products, recombination mod q2
+    // inverses on X0, X1, X0, X1, rounding to the exact limb products, recombination mod q2
 #pragma unroll
     for (int o = 0; o < 2; ++o) {
 #pragma unroll
-      for (int l = 0; l < 2; ++l) F::inv(sr[o][l], si[o][l], Xb[1 - l], W, tws, t);
-#pragma unroll
-      for (int e = 0; e < E; ++e)
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const double ylo = h ? si[o][0][e] : sr[o][0][e], yhi = h ? si[o][1][e] : sr[o][1][e];
-          const double lo = rint(ylo), hr = rint(yhi);
-          rg.note(ylo, lo);
-          rg.note(yhi, hr);
-          const double hi = hr * LIMB;  // exact (|P_hi| < 2^45)
-          ac[o][h][e] = canon<M>(ac[o][h][e] + red<M>(hi) + lo);
-        }
+      for (int l = 0; l < 2; ++l) F::inv(sr[o][l], si[o][l], Xb[l], tws, t, w3, w4);
+      br2f_update<G>(acs + o * NN, sr[o], si[o], rg, t);
     }
   }
   rg.publish(margin);
+  __syncthreads();  // the last updates everywhere
   uint64_t *o = out + (size_t)blockIdx.x * 2 * NN;
   if (mode == 1) {
 #pragma unroll
@@ -516,26 +509,21 @@ __device__ __forceinline__ void br2f_body(const uint32_t *__restrict__ lwe_int, 
 #pragma unroll
       for (int h = 0; h < 2; ++h)
 #pragma unroll
-        for (int e = 0; e < E; ++e) o[p * NN + F::idx(0, t, e) + F::n * h] = to_u64<M>(ac[p][h][e]);
+        for (int e = 0; e < E; ++e) {
+          const int c = F::idx(0, t, e) + F::n * h;
+          o[p * NN + c] = to_u64<M>(acs[p * NN + F::slot_stage(c)]);
+        }
     return;
   }
   // hom_trace on the accumulator in the trace NTTs' coefficient layout (t + 256 e, 8 per thread)
-  double *xch = reinterpret_cast<double *>(&lds2[0][0]);  // 3 N2 doubles
-  double *tw = reinterpret_cast<double *>(tws);           // N2 doubles
-  __syncthreads();  // the last inverse's reads are done everywhere
-#pragma unroll
-  for (int p = 0; p < 2; ++p)
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int e = 0; e < E; ++e) xch[p * NN + F::idx(0, t, e) + F::n * h] = ac[p][h][e];
-  __syncthreads();
   double acc0[BR2_E], acc1[BR2_E];
 #pragma unroll
   for (int e = 0; e < BR2_E; ++e) {
-    acc0[e] = xch[t + e * BR2_T];
-    acc1[e] = xch[NN + t + e * BR2_T];
+    acc0[e] = acs[F::slot_stage(t + e * BR2_T)];
+    acc1[e] = acs[NN + F::slot_stage(t + e * BR2_T)];
   }
+  double *xch = reinterpret_cast<double *>(&lds[0][0]);  // 3 N2 doubles
+  double *tw = reinterpret_cast<double *>(tws);           // N2 doubles
   __syncthreads();
 #pragma unroll
   for (int e = 0; e < BR2_E; ++e) {
