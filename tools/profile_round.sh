@@ -22,11 +22,11 @@ run 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_
 run 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_LDS SQ_INSTS_SALU SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_ANY SQ_WAIT_INST_LDS -T -f csv -d $out/pmc2 -o pmc -- python $B
 run 300 python bench.py --messages 4096 --steps 1 --warmup 1 --force-dist --no-cpu-baseline > $out/bench_forcedist_rccl_n1.json 2> $out/forcedist.err
 tail -1 $out/bench_forcedist_rccl_n1.json
-# last: a process that made cooperative launches (the latency path's two-CU / five-CU kernels)
-# faults at exit under rocprofv3: libamdhip64's exit handler -> libhsa-runtime64 teardown, after the
-# profiler tool has finalised (its trace and stats are complete). Not this library's code: the same
-# workload without cooperative launches (OMR_COOPERATIVE=0 or threshold 0) exits 0, with torch's
-# bundled HIP runtime it faults the same way, and hipDeviceReset before exit does not avoid it
-# (profiles/r04/exit_fault_*). So nothing runs after it.
-run 300 rocprofv3 --kernel-trace --stats -T -f csv -d $out/kt_latency -o kt -- python tools/latency_split.py 1 7
+# The single-message latency split as it runs (cooperative two-CU / five-CU kernels), unprofiled,
+# then its kernel trace with OMR_COOPERATIVE=0 (br2l / trace_kernel instead of br2x / trace_x): a
+# profiled process that made a cooperative launch faults in the HIP/HSA runtime's exit-time teardown
+# after the tool has finalised (tools/coop_min.hip reproduces it with no library state,
+# profiles/r05/coop_min_exit_fault.md), so the profiled step avoids them and the round exits 0.
+run 300 python tools/latency_split.py 1 7 > $out/latency_split.log
+OMR_COOPERATIVE=0 run 300 rocprofv3 --kernel-trace --stats -T -f csv -d $out/kt_latency -o kt -- python tools/latency_split.py 1 7
 find $out -name "*.csv" | head -30
