@@ -17,7 +17,6 @@
 #include <vector>
 
 #include "br2_fft.hpp"
-#include "br2_sched.hpp"
 #include "detect_kernels.hpp"
 #include "encode_kernels.hpp"
 #include "key_spectra.hpp"
@@ -330,18 +329,7 @@ struct omr_ctx {
 
 #define OMR_BR1_NAME "br1f_kernel"
 #define OMR_KS_NAME "ks_mfma_kernel"
-#ifndef OMR_BR2_SCHED
-#define OMR_BR2_SCHED 0  // 1: br2s_kernel (br2_sched.hpp, experiment)
-#endif
-#if OMR_BR2_SCHED
-#define OMR_BR2_NAME "br2s_kernel"
-#define OMR_BR2_KERNEL br2s_kernel
-#define OMR_BR2_GUARD_KERNEL br2s_guard_kernel
-#else
 #define OMR_BR2_NAME "br2f_kernel"
-#define OMR_BR2_KERNEL br2f_kernel
-#define OMR_BR2_GUARD_KERNEL br2f_guard_kernel
-#endif
 
 namespace {
 
@@ -652,7 +640,7 @@ omr_status launch_br2(omr_ctx *c, size_t n, const uint32_t *lwe_int, uint64_t *o
       // (br2l_fallback_kernel: every workgroup leaves at once otherwise), its trace too when fused
       omr_status s;
       if ((s = guard_begin(c, 1, st)) != OMR_OK) return s;
-      OMR_BR2_GUARD_KERNEL<<<(unsigned)n, Fft1024::T, 0, st>>>(lwe_int, c->bsk2f, c->fft2, c->tk, c->tb, out, m,
+      br2f_guard_kernel<<<(unsigned)n, Fft1024::T, 0, st>>>(lwe_int, c->bsk2f, c->fft2, c->tk, c->tb, out, m,
                                                             c->margin + 3);
       HIP_TRY(hipGetLastError());
       br2l_fallback_kernel<<<(unsigned)n, BR2L_T, 0, st>>>(lwe_int, c->bsk2, c->tb, out, c->margin + 3, c->thr[1]);
@@ -662,7 +650,7 @@ omr_status launch_br2(omr_ctx *c, size_t n, const uint32_t *lwe_int, uint64_t *o
       HIP_TRY(hipGetLastError());
       if ((s = guard_end(c, 1, st)) != OMR_OK) return s;
     } else {
-      OMR_BR2_KERNEL<<<(unsigned)n, Fft1024::T, 0, st>>>(lwe_int, c->bsk2f, c->fft2, c->tk, c->tb, out, m);
+      br2f_kernel<<<(unsigned)n, Fft1024::T, 0, st>>>(lwe_int, c->bsk2f, c->fft2, c->tk, c->tb, out, m);
     }
   }
   HIP_TRY(hipGetLastError());
