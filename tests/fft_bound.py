@@ -3,10 +3,10 @@ from the coefficient-domain key with numpy -- the same formula context.hip's apr
 evaluates on the device-stored double-double key spectra at context creation:
 
   E = n D (1 + 2^-30) max over steps i and output spectra o of
-      [(2 delta_f + u (1 + 2^-40)) sum_r kappa_{i,r,o} + sqrt(2) u sum_k (2R - 2k) kappa_{i,r(k),o}]
+      [(delta_fwd + delta_inv + u (1 + 2^-40)) sum_r kappa_{i,r,o} + sqrt(2) u sum_k (2R - 2k) kappa_{i,r(k),o}]
 
 n complex points, R GGSW rows accumulated in the order r(0), r(1), ..., D = sqrt(2n) d_max,
-delta_f = 26u, kappa_{i,r,o} = max_j |K_{i,r,o}[j]| (spectrum of key row r of step i, output o;
+delta_fwd + delta_inv = 37u + 32u (level 1: tangent-form forward butterflies) or 26u + 26u (level 2), kappa_{i,r,o} = max_j |K_{i,r,o}[j]| (spectrum of key row r of step i, output o;
 level 2: per 25-bit limb). Spectral magnitudes do not depend on the output order, so a plain
 twisted DFT gives them: K[m] = (1/n) sum_k z_k e^{i pi k / 2n} e^{2 pi i k m / n}."""
 import numpy as np
@@ -26,11 +26,11 @@ def _row_max(rows, n):
     return np.abs(np.fft.fft(z * tw, axis=-1)).max(axis=-1) / n
 
 
-def _bound(kmax, n, R, dmax, order):
-    """kmax [steps][R][outputs]"""
+def _bound(kmax, n, R, dmax, order, dft):
+    """kmax [steps][R][outputs]; dft = (delta_fwd + delta_inv) / u"""
     k = kmax[:, order, :]
     w = (2.0 * R - 2.0 * np.arange(R))[None, :, None]
-    inner = (2 * 26 * U + U * (1 + 2.0 ** -40)) * k.sum(axis=1) + np.sqrt(2.0) * U * (w * k).sum(axis=1)
+    inner = (dft * U + U * (1 + 2.0 ** -40)) * k.sum(axis=1) + np.sqrt(2.0) * U * (w * k).sum(axis=1)
     return n * np.sqrt(2.0 * n) * dmax * inner.max() * (1 + 2.0 ** -30)
 
 
@@ -41,6 +41,6 @@ def apriori_bounds(dk, q1=134215681, q2=1125899906826241):
     r2 = _centred(dk.bsk2.reshape(670, 12, 2, 2048), q2)
     hi = np.rint(r2 / 2.0 ** 25)
     k2 = np.stack([_row_max(r2 - hi * 2.0 ** 25, 1024), _row_max(hi, 1024)], axis=-1).reshape(670, 12, 4)
-    e1 = _bound(k1, 512, 8, 16.0, list(range(8)))
-    e2 = _bound(k2, 1024, 12, 64.0, ORDER2)
+    e1 = _bound(k1, 512, 8, 16.0, list(range(8)), 37 + 32)
+    e2 = _bound(k2, 1024, 12, 64.0, ORDER2, 26 + 26)
     return e1, e2, float(k1.max()), float(k2.max())

@@ -1,12 +1,15 @@
 """Level-1 FFT layout (tfhe-omr_amd/csrc/device_fft.hpp, WgFft::jidx / slot, restated here): the
 four pass layouts are bijections, the permlane swaps (register bits 2, 1 <-> lane bits 5, 4 after
 pass 0; register bit 2 <-> lane bit 5 after pass 2) produce the next pass's layout, the one LDS
-exchange is bank-conflict free in both directions, and the numpy model of the kernel's pass
-structure (tools/fft_exactness.py, Fft8P) returns the exact negacyclic product after rounding."""
+exchange is bank-conflict free in both directions, and the numpy models of the kernel's pass
+structure (tools/fft_exactness.py: Fft8P, the premultiplied passes of rounds 2-4; Fft8PT, the
+tangent-form forward butterflies of round 5) return the exact negacyclic product after rounding,
+and agree with each other to rounding."""
 import os
 import sys
 
 import numpy as np
+import pytest
 
 sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "tools"))
 import fft_exactness as FX  # noqa: E402
@@ -69,8 +72,9 @@ def test_exchange_conflict_free():
                 assert len(set((r[g] % 16).tolist())) == 16
 
 
-def test_model_exact_product():
-    f = FX.Fft8P()
+@pytest.mark.parametrize("model", ["Fft8P", "Fft8PT"])
+def test_model_exact_product(model):
+    f = getattr(FX, model)()
     for lane_e in [(p, e) for p in range(4) for e in range(8)]:
         assert np.array_equal(f.jidx(*lane_e), jidx(lane_e[0], LANE, lane_e[1]))
     rng = np.random.default_rng(3)
@@ -83,3 +87,12 @@ def test_model_exact_product():
         out = FX.unfold(f.inv(acc))
         assert np.array_equal(np.rint(out), exact)
         assert np.max(np.abs(out - exact)) < 0.01
+
+
+def test_tangent_model_matches_premultiplied():
+    rng = np.random.default_rng(11)
+    z = rng.standard_normal(512) + 1j * rng.standard_normal(512)
+    a, b = FX.Fft8P(), FX.Fft8PT()
+    fa, fb = a.fwd(z), b.fwd(z)
+    assert np.max(np.abs(fa - fb)) < 1e-12 * np.max(np.abs(fa))
+    assert np.max(np.abs(b.inv(fb) / 512 - z)) < 1e-12

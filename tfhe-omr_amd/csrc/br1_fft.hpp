@@ -324,7 +324,7 @@ __device__ __forceinline__ void br1f_body(
   // pass 3's two lane twiddles in registers for the whole rotation: 2 KB of LDS reads fewer per
   // transform (LDS runs at ~60 % of its bandwidth here; 595 -> 591 ms per 16,384 messages,
   // profiles/r04/br1f_w3_ab.log)
-  const double2 w3[2] = {tws[255 + lane], tws[255 + 64 + lane]};
+  const double2 w3[2] = {tws[Fft512::TW_P3 + lane], tws[Fft512::TW_P3 + 64 + lane]};
   // every step runs (a = 0 gives zero digits and leaves ACC unchanged) so the waves share the
   // staged key rows; row 0 is issued before the loop
   const __amdgpu_buffer_rsrc_t rsrc = bsk1_rsrc(bskf);

@@ -78,14 +78,17 @@ std::vector<double> negacyclic_lut(const std::vector<uint64_t> &v, int N, int lo
 
 // FFT twiddles of Fft512 (device_fft.hpp, WgFft): node i of stage s -> w^(eps(s, i) / 2),
 // w = exp(i pi / 2n), n = 512, eps(0, 0) = n, eps(s+1, 2i) = eps(s, i) / 2,
-// eps(s+1, 2i+1) = eps(s, i) / 2 + 2n (mod 4n). Layout (WgFft): [0, 7) T_1..T_7 of the pass-0
-// radix-8 block (A = node(0, 0), B = node(1, 0), C = node(2, 0), T = (C, B, BC, A, AC, AB, ABC));
-// 7 + 3 blk + (B, A, AB) of the pass-1 radix-4 block blk (A = node(3, blk), B = node(4, 2 blk));
-// 31 + (t - 1) 32 + hi the pass-2 radix-8 blocks (A = node(5, hi), B = node(6, 2 hi),
-// C = node(7, 4 hi)); 255 + 64 e1 + lane the pass-3 (stage 8) even-sibling node
+// eps(s+1, 2i+1) = eps(s, i) / 2 + 2n (mod 4n). Layout (WgFft::TW_*): [0, 7) T_1..T_7 of the
+// pass-0 radix-8 block (A = node(0, 0), B = node(1, 0), C = node(2, 0), T = (C, B, BC, A, AC, AB,
+// ABC)), inverse only; [7, 11) the tangent forms (cos, tan) of pass 0's A, B, C, w8 C = node(2, 2);
+// 11 + 2 blk + (A, B) the tangent forms of the pass-1 radix-4 block blk (A = node(3, blk),
+// B = node(4, 2 blk)); 27 + (t - 1) 32 + hi the pass-2 T_t (A = node(5, hi), B = node(6, 2 hi),
+// C = node(7, 4 hi)), inverse only; 251 + 32 k + hi the tangent forms of pass 2's A, B, C, w8 C;
+// 379 + 64 e1 + lane the tangent form of the pass-3 (stage 8) even-sibling node
 // ((lane & 31) << 3 | (lane >> 5) << 2 | e1 << 1). Each entry is an exact angle (sum of the nodes'
-// integer half-eps) evaluated in long double and rounded once.
+// integer half-eps) evaluated in long double and rounded once (tan = sin / cos in long double).
 std::vector<double2> fft_twiddles() {
+  using F = Fft512;
   const int L = 9, n = 1 << L;
   std::vector<double2> tw(n, make_double2(1.0, 0.0));
   std::vector<std::vector<long>> half(L);  // half[s][i] = eps(s, i) / 2
@@ -99,26 +102,36 @@ std::vector<double2> fft_twiddles() {
     }
     eps.swap(next);
   }
-  auto at = [&](long h) {
-    const long double ang = 3.14159265358979323846264338327950288L * (long double)(h % (8 * n)) / (long double)(2 * n);
-    return make_double2((double)cosl(ang), (double)sinl(ang));
+  auto angle = [&](long h) {
+    return 3.14159265358979323846264338327950288L * (long double)(h % (8 * n)) / (long double)(2 * n);
+  };
+  auto at = [&](long h) { return make_double2((double)cosl(angle(h)), (double)sinl(angle(h))); };
+  auto ct = [&](long h) {  // no node of the tree lies on an axis, so cos != 0
+    const long double c = cosl(angle(h)), s = sinl(angle(h));
+    return make_double2((double)c, (double)(s / c));
   };
   auto radix8 = [&](int s0, int hi, auto put) {
     const long a = half[s0][hi], b = half[s0 + 1][2 * hi], c = half[s0 + 2][4 * hi];
     const long h[8] = {0, c, b, b + c, a, a + c, a + b, a + b + c};
     for (int t = 1; t < 8; ++t) put(t, at(h[t]));
   };
-  radix8(0, 0, [&](int t, double2 v) { tw[t - 1] = v; });
+  auto radix8_ct = [&](int s0, int hi, auto put) {
+    const long h[4] = {half[s0][hi], half[s0 + 1][2 * hi], half[s0 + 2][4 * hi], half[s0 + 2][4 * hi + 2]};
+    for (int k = 0; k < 4; ++k) put(k, ct(h[k]));
+  };
+  radix8(0, 0, [&](int t, double2 v) { tw[F::TW_P0I + t - 1] = v; });
+  radix8_ct(0, 0, [&](int k, double2 v) { tw[F::TW_P0F + k] = v; });
   for (int blk = 0; blk < 8; ++blk) {
-    const long a = half[3][blk], b = half[4][2 * blk];
-    tw[7 + 3 * blk] = at(b);
-    tw[7 + 3 * blk + 1] = at(a);
-    tw[7 + 3 * blk + 2] = at(a + b);
+    tw[F::TW_P1 + 2 * blk] = ct(half[3][blk]);
+    tw[F::TW_P1 + 2 * blk + 1] = ct(half[4][2 * blk]);
   }
-  for (int hi = 0; hi < 32; ++hi) radix8(5, hi, [&](int t, double2 v) { tw[31 + (t - 1) * 32 + hi] = v; });
+  for (int hi = 0; hi < 32; ++hi) {
+    radix8(5, hi, [&](int t, double2 v) { tw[F::TW_P2I + (t - 1) * 32 + hi] = v; });
+    radix8_ct(5, hi, [&](int k, double2 v) { tw[F::TW_P2F + k * 32 + hi] = v; });
+  }
   for (int e1 = 0; e1 < 2; ++e1)
     for (int lane = 0; lane < 64; ++lane)
-      tw[255 + 64 * e1 + lane] = at(half[8][((lane & 31) << 3) | ((lane >> 5) << 2) | (e1 << 1)]);
+      tw[F::TW_P3 + 64 * e1 + lane] = ct(half[8][((lane & 31) << 3) | ((lane >> 5) << 2) | (e1 << 1)]);
   return tw;
 }
 
@@ -210,9 +223,11 @@ std::vector<CDD> dd_tree_twiddles(int L) {
 // (DESIGN.md §3a). For one CMUX step and one output spectrum, with n complex points, D =
 // sqrt(2n) d_max the 2-norm bound of a digit polynomial, kappa_r the largest |K^| of GGSW row r
 // (row_max_abs_kernel), the rows accumulated in the order r(0), r(1), ... by two fmas each:
-//   E = n D (1 + 2^-30) [(2 delta_f + u (1 + 2^-40)) sum_r kappa_r + sqrt(2) u sum_k (2R - 2k) kappa_r(k)]
-// forward digit transforms and the inverse each within delta_f = 26u relative 2-norm error (5u per
-// radix-4 pass, 8u per radix-8, 4u per radix-2, rounded up), the sequential fma accumulation, and
+//   E = n D (1 + 2^-30) [(delta_fwd + delta_inv + u (1 + 2^-40)) sum_r kappa_r + sqrt(2) u sum_k (2R - 2k) kappa_r(k)]
+// the forward digit transforms within delta_fwd and the inverse within delta_inv relative 2-norm
+// error (level 2, premultiplied radix-4 passes: 26u each; level 1: 37u forward -- 4u per
+// tangent-form radix-2 stage, 9 stages -- and 32u inverse -- 8u per premultiplied radix-8 pass,
+// 5u per Gentleman-Sande stage of P1 and P3 -- rounded up), the sequential fma accumulation, and
 // the double-double keys' |K^ - K| <= u |K|. The maximum over every step and output spectrum.
 // kmax: [steps][rows][outputs] (level 1: [512][8][2]; level 2: [670][12][2 out][2 limb], the limbs
 // as two more "outputs").
@@ -224,7 +239,8 @@ double apriori_bound(int level, const std::vector<double> &kmax) {
   // g = 2 j + w, row p D2 + j + 3 w (br2_fft.hpp)
   const int order2[12] = {0, 3, 1, 4, 2, 5, 6, 9, 7, 10, 8, 11};
   const double D = std::sqrt(2.0 * n) * (level == 1 ? 16.0 : 64.0);
-  const double cf = 2 * 26 * u + u * (1 + 0x1p-40), cw = std::sqrt(2.0) * u;
+  const double dft = level == 1 ? 37 + 32 : 26 + 26;  // delta_fwd + delta_inv, in units of u
+  const double cf = dft * u + u * (1 + 0x1p-40), cw = std::sqrt(2.0) * u;
   double worst = 0.0;
   for (int i = 0; i < steps; ++i)
     for (int o = 0; o < O; ++o) {

@@ -48,22 +48,34 @@ __device__ __forceinline__ void wave_lds_fence() {
 //   P3: e2 -> j0, e1 -> j2, e0 -> j1; lane 5 -> j3, lane 4..0 -> j8..j4
 //       (P2 -> P3: register bit 2 <-> lane bit 5, permlane)
 // P0 and P2 are radix-8 blocks of the twiddle tree: the block's stage-s0 node (hi) has twiddle A,
-// its children B, i B and grandchildren C, i C, w8 C, i w8 C (w8 = exp(i pi / 4)); three radix-2
-// stages equal "x_e *= T_e, then a constant 8-point network" with T = (1, C, B, BC, A, AC, AB, ABC):
-// 80 FP64 operations instead of 96 (the factors i free, w8 folded into FMAs). P1 is two radix-4
-// blocks (register bit 0 = j6 selects the block): T = (1, B, A, AB) on registers (e0, e0 + 2,
-// e0 + 4, e0 + 6), 3 products + 8 additions. P3 is one radix-2 stage, odd siblings (register bit
-// 0 = j1) taking i w. tools/fft_exactness.py (Fft8P) models this structure against the exact
-// negacyclic product. The exchange replaced by the permlane relayouts cost 14 % of the level-1
-// kernel (timing ablation).
-// Twiddle table (double2): [0, 7) T_1..T_7 of P0 (wave-uniform); 7 + 3 blk + (B, A, AB) of P1's
-// block blk = (j8 j7 j6); 31 + (t - 1) 32 + hi, hi = j8..j4 = lane & 31, for P2; 255 + 64 e1 + lane
-// for P3's stage-8 twiddle of the even sibling.
+// its children B, i B and grandchildren C, i C, w8 C, i w8 C (w8 = exp(i pi / 4)). P1 is two
+// radix-4 blocks (register bit 0 = j6 selects the block; A, then B and i B on registers (e0,
+// e0 + 2, e0 + 4, e0 + 6)). P3 is one radix-2 stage, odd siblings (register bit 0 = j1) taking i w.
+// Forward passes: radix-2 butterflies in tangent form (round 5): a twiddle w = c (1 + i t) stored
+// as (c, t = tan), (p, q) -> (p + c u, p - c u) with u = q (1 + i t): 6 FMAs per butterfly instead
+// of a complex product and 4 additions (8), and a factor i only permutes the last 4 FMAs' operands,
+// so a block needs the (c, t) of A, B, C, w8 C alone. A radix-8 pass is 72 FP64 operations instead
+// of the premultiplied form's 80 ("x_e *= T_e, then a constant network", T = (1, C, B, BC, A, AC,
+// AB, ABC)), a radix-4 block 24 instead of 28, the radix-2 pass 24 instead of 32: 216 per
+// transform instead of 248 (DESIGN.md §3a bounds the error, 4u per stage). Inverse passes: the
+// radix-8 ones keep the premultiplied adjoint (80 operations; a Gentleman-Sande butterfly subtracts
+// before it multiplies, so the tangent form saves nothing there), P1 and P3 use the (c, t) tree
+// (conj(w) d = c (d (1 - i t))), which shares their table with the forward.
+// tools/fft_exactness.py (Fft8P, Fft8PT) models both structures against the exact negacyclic
+// product. The exchange replaced by the permlane relayouts cost 14 % of the level-1 kernel
+// (timing ablation).
+// Twiddle table (double2; WgFft::TW_*): [0, 7) T_1..T_7 of P0 (wave-uniform, inverse); [7, 11) (c, t)
+// of P0's A, B, C, w8 C; 11 + 2 blk + (A, B) (c, t) of P1's block blk = (j8 j7 j6); 27 + (t - 1) 32
+// + hi, hi = j8..j4 = lane & 31, P2's T_t (inverse); 251 + 32 k + hi the (c, t) of P2's A, B, C,
+// w8 C; 379 + 64 e1 + lane the (c, t) of P3's stage-8 twiddle of the even sibling.
 template <int T_, int E_, int L_>
 struct WgFft {
   static constexpr int T = T_, E = E_, L = L_, N = T * E;
   static_assert(T == 64 && E == 8 && L == 9, "written for the level-1 geometry: one wave, 64 x 8");
   static constexpr int BUF = N;  // LDS slots (double2) per transform
+  // twiddle table offsets (double2 entries; fft_twiddles() in context.hip writes them)
+  static constexpr int TW_P0I = 0, TW_P0F = 7, TW_P1 = 11, TW_P2I = 27, TW_P2F = 251, TW_P3 = 379, TW_LEN = 507;
+  static_assert(TW_LEN <= N, "the table is copied to an N-entry LDS array");
 
   __device__ static __forceinline__ int jidx(int p, int lane, int e) {
     const int l5 = (lane >> 5) & 1, l4 = (lane >> 4) & 1;
@@ -136,66 +148,76 @@ struct WgFft {
 
   static constexpr double S8 = 0.70710678118654752440;  // 1 / sqrt(2), w8 = S8 (1 + i)
 
-  // radix-8 block twiddle T_t (t = 1..7) of pass P in {0, 2}; pass 0 from the global table with
-  // wave-uniform (scalar) loads when G
+  // radix-8 block twiddle T_t (t = 1..7) of pass P in {0, 2} (inverse); pass 0 from the global
+  // table with wave-uniform (scalar) loads when G
   template <int P, bool G>
   __device__ static __forceinline__ double2 tw8(const double2 *tws, const double2 *__restrict__ gtw, int t,
                                                 int lane) {
-    if constexpr (P == 0) return G ? gtw[t - 1] : tws[t - 1];
-    return tws[31 + (t - 1) * 32 + (lane & 31)];
+    if constexpr (P == 0) return G ? gtw[TW_P0I + t - 1] : tws[TW_P0I + t - 1];
+    return tws[TW_P2I + (t - 1) * 32 + (lane & 31)];
+  }
+  // (c, t) of the radix-8 block's A, B, C, w8 C (k = 0..3), pass P in {0, 2} (forward)
+  template <int P, bool G>
+  __device__ static __forceinline__ double2 ct8(const double2 *tws, const double2 *__restrict__ gtw, int k,
+                                                int lane) {
+    if constexpr (P == 0) return G ? gtw[TW_P0F + k] : tws[TW_P0F + k];
+    return tws[TW_P2F + k * 32 + (lane & 31)];
+  }
+
+  // forward radix-2 butterfly in tangent form: (p, q) <- (p + w q, p - w q), w = c (1 + i t);
+  // I: the node's twiddle is i w
+  template <bool I>
+  __device__ static __forceinline__ void bfly(double &pr, double &pi, double &qr, double &qi, double c, double t) {
+    const double ur = __fma_rn(-t, qi, qr), ui = __fma_rn(t, qr, qi);  // u = q (1 + i t), w q = c u
+    const double ar = pr, ai = pi;
+    if constexpr (!I) {
+      pr = __fma_rn(c, ur, ar);
+      pi = __fma_rn(c, ui, ai);
+      qr = __fma_rn(-c, ur, ar);
+      qi = __fma_rn(-c, ui, ai);
+    } else {  // i c u = c (-ui + i ur)
+      pr = __fma_rn(-c, ui, ar);
+      pi = __fma_rn(c, ur, ai);
+      qr = __fma_rn(c, ui, ar);
+      qi = __fma_rn(-c, ur, ai);
+    }
+  }
+  // its unscaled inverse (Gentleman-Sande): (p, q) <- (p + q, conj(w) (p - q)); conj(i w) = -i conj(w)
+  template <bool I>
+  __device__ static __forceinline__ void ibfly(double &pr, double &pi, double &qr, double &qi, double c, double t) {
+    const double dr = pr - qr, di = pi - qi;
+    pr = pr + qr;
+    pi = pi + qi;
+    const double vr = __fma_rn(t, di, dr), vi = __fma_rn(-t, dr, di);  // v = d (1 - i t), conj(w) d = c v
+    if constexpr (!I) {
+      qr = c * vr;
+      qi = c * vi;
+    } else {  // -i c v = c (vi - i vr)
+      qr = c * vi;
+      qi = -c * vr;
+    }
   }
 
   template <int P, int C, bool G = false>
   __device__ static __forceinline__ void fwd8(double (&xr)[C][E], double (&xi)[C][E], const double2 *tws,
                                               int lane, const double2 *__restrict__ gtw = nullptr) {
-    double2 wt[8];  // the block's twiddles, all requested before the first use (one LDS round trip)
+    double2 ct[4];  // (c, t) of A, B, C, w8 C, all requested before the first use (one LDS round trip)
 #pragma unroll
-    for (int t = 1; t < 8; ++t) wt[t] = tw8<P, G>(tws, gtw, t, lane);
+    for (int k = 0; k < 4; ++k) ct[k] = ct8<P, G>(tws, gtw, k, lane);
     if constexpr (P != 0) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int t = 1; t < 8; ++t) {  // x_t *= T_t
-      const double2 w = wt[t];
-#pragma unroll
-      for (int c = 0; c < C; ++c) {
-        const double r = __fma_rn(xr[c][t], w.x, -xi[c][t] * w.y);
-        const double i = __fma_rn(xr[c][t], w.y, xi[c][t] * w.x);
-        xr[c][t] = r;
-        xi[c][t] = i;
-      }
-    }
-#pragma unroll
     for (int c = 0; c < C; ++c) {
-      double ar[4], ai[4], br[4], bi[4];
+      double *r = xr[c], *i = xi[c];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        ar[e] = xr[c][e] + xr[c][e + 4];
-        ai[e] = xi[c][e] + xi[c][e + 4];
-        br[e] = xr[c][e] - xr[c][e + 4];
-        bi[e] = xi[c][e] - xi[c][e + 4];
-      }
-      // c = a0 +- a2, a1 +- a3; d = b0 +- i b2, b1 +- i b3
-      const double c0r = ar[0] + ar[2], c0i = ai[0] + ai[2], c2r = ar[0] - ar[2], c2i = ai[0] - ai[2];
-      const double c1r = ar[1] + ar[3], c1i = ai[1] + ai[3], c3r = ar[1] - ar[3], c3i = ai[1] - ai[3];
-      const double d0r = br[0] - bi[2], d0i = bi[0] + br[2], d2r = br[0] + bi[2], d2i = bi[0] - br[2];
-      const double d1r = br[1] - bi[3], d1i = bi[1] + br[3], d3r = br[1] + bi[3], d3i = bi[1] - br[3];
-      xr[c][0] = c0r + c1r;
-      xi[c][0] = c0i + c1i;
-      xr[c][1] = c0r - c1r;
-      xi[c][1] = c0i - c1i;
-      xr[c][2] = c2r - c3i;  // c2 + i c3
-      xi[c][2] = c2i + c3r;
-      xr[c][3] = c2r + c3i;  // c2 - i c3
-      xi[c][3] = c2i - c3r;
-      const double u = d1r - d1i, v = d1r + d1i;  // w8 d1 = S8 (u + i v)
-      xr[c][4] = __fma_rn(S8, u, d0r);
-      xi[c][4] = __fma_rn(S8, v, d0i);
-      xr[c][5] = __fma_rn(-S8, u, d0r);
-      xi[c][5] = __fma_rn(-S8, v, d0i);
-      const double u3 = d3r + d3i, v3 = d3r - d3i;  // i w8 d3 = S8 (-u3 + i v3)
-      xr[c][6] = __fma_rn(-S8, u3, d2r);
-      xi[c][6] = __fma_rn(S8, v3, d2i);
-      xr[c][7] = __fma_rn(S8, u3, d2r);
-      xi[c][7] = __fma_rn(-S8, v3, d2i);
+      for (int e = 0; e < 4; ++e) bfly<false>(r[e], i[e], r[e + 4], i[e + 4], ct[0].x, ct[0].y);  // A
+      bfly<false>(r[0], i[0], r[2], i[2], ct[1].x, ct[1].y);  // B
+      bfly<false>(r[1], i[1], r[3], i[3], ct[1].x, ct[1].y);
+      bfly<true>(r[4], i[4], r[6], i[6], ct[1].x, ct[1].y);  // i B
+      bfly<true>(r[5], i[5], r[7], i[7], ct[1].x, ct[1].y);
+      bfly<false>(r[0], i[0], r[1], i[1], ct[2].x, ct[2].y);  // C
+      bfly<true>(r[2], i[2], r[3], i[3], ct[2].x, ct[2].y);   // i C
+      bfly<false>(r[4], i[4], r[5], i[5], ct[3].x, ct[3].y);  // w8 C
+      bfly<true>(r[6], i[6], r[7], i[7], ct[3].x, ct[3].y);   // i w8 C
     }
   }
   // unscaled inverse of fwd8 (8 x its inverse): the adjoint network, then x_e *= conj(T_e)
@@ -254,31 +276,23 @@ struct WgFft {
     }
   }
 
-  // P1: two radix-4 blocks
-  __device__ static __forceinline__ int tw4_index(int lane, int e0, int k) {  // k: 0 B, 1 A, 2 AB
-    return 7 + 3 * ((((lane >> 4) & 3) << 1) | e0) + k;
+  // P1: two radix-4 blocks, (c, t) of A and B per block
+  __device__ static __forceinline__ int tw4_index(int lane, int e0, int k) {  // k: 0 A, 1 B
+    return TW_P1 + 2 * ((((lane >> 4) & 3) << 1) | e0) + k;
   }
   template <int C>
   __device__ static __forceinline__ void fwd4(double (&xr)[C][E], double (&xi)[C][E], const double2 *tws, int lane) {
 #pragma unroll
     for (int e0 = 0; e0 < 2; ++e0) {
-      const double2 B = tws[tw4_index(lane, e0, 0)], A = tws[tw4_index(lane, e0, 1)], AB = tws[tw4_index(lane, e0, 2)];
+      const double2 A = tws[tw4_index(lane, e0, 0)], B = tws[tw4_index(lane, e0, 1)];
+      const int r0 = e0, r1 = e0 | 2, r2 = e0 | 4, r3 = e0 | 6;
 #pragma unroll
       for (int c = 0; c < C; ++c) {
-        const int r0 = e0, r1 = e0 | 2, r2 = e0 | 4, r3 = e0 | 6;
-        const double p1r = __fma_rn(xr[c][r1], B.x, -xi[c][r1] * B.y), p1i = __fma_rn(xr[c][r1], B.y, xi[c][r1] * B.x);
-        const double p2r = __fma_rn(xr[c][r2], A.x, -xi[c][r2] * A.y), p2i = __fma_rn(xr[c][r2], A.y, xi[c][r2] * A.x);
-        const double p3r = __fma_rn(xr[c][r3], AB.x, -xi[c][r3] * AB.y), p3i = __fma_rn(xr[c][r3], AB.y, xi[c][r3] * AB.x);
-        const double a0r = xr[c][r0] + p2r, a0i = xi[c][r0] + p2i, b0r = xr[c][r0] - p2r, b0i = xi[c][r0] - p2i;
-        const double a1r = p1r + p3r, a1i = p1i + p3i, b1r = p1r - p3r, b1i = p1i - p3i;
-        xr[c][r0] = a0r + a1r;
-        xi[c][r0] = a0i + a1i;
-        xr[c][r1] = a0r - a1r;
-        xi[c][r1] = a0i - a1i;
-        xr[c][r2] = b0r - b1i;  // b0 + i b1
-        xi[c][r2] = b0i + b1r;
-        xr[c][r3] = b0r + b1i;  // b0 - i b1
-        xi[c][r3] = b0i - b1r;
+        double *r = xr[c], *i = xi[c];
+        bfly<false>(r[r0], i[r0], r[r2], i[r2], A.x, A.y);
+        bfly<false>(r[r1], i[r1], r[r3], i[r3], A.x, A.y);
+        bfly<false>(r[r0], i[r0], r[r1], i[r1], B.x, B.y);
+        bfly<true>(r[r2], i[r2], r[r3], i[r3], B.x, B.y);
       }
     }
   }
@@ -286,68 +300,49 @@ struct WgFft {
   __device__ static __forceinline__ void inv4(double (&xr)[C][E], double (&xi)[C][E], const double2 *tws, int lane) {
 #pragma unroll
     for (int e0 = 0; e0 < 2; ++e0) {
-      const double2 B = tws[tw4_index(lane, e0, 0)], A = tws[tw4_index(lane, e0, 1)], AB = tws[tw4_index(lane, e0, 2)];
+      const double2 A = tws[tw4_index(lane, e0, 0)], B = tws[tw4_index(lane, e0, 1)];
+      const int r0 = e0, r1 = e0 | 2, r2 = e0 | 4, r3 = e0 | 6;
 #pragma unroll
       for (int c = 0; c < C; ++c) {
-        const int r0 = e0, r1 = e0 | 2, r2 = e0 | 4, r3 = e0 | 6;
-        const double sr = xr[c][r0] + xr[c][r1], si = xi[c][r0] + xi[c][r1];
-        const double tr = xr[c][r0] - xr[c][r1], ti = xi[c][r0] - xi[c][r1];
-        const double ur = xr[c][r2] + xr[c][r3], ui = xi[c][r2] + xi[c][r3];
-        const double vr = xi[c][r2] - xi[c][r3], vi = xr[c][r3] - xr[c][r2];  // -i (o2 - o3)
-        const double p1r = tr + vr, p1i = ti + vi, p2r = sr - ur, p2i = si - ui, p3r = tr - vr, p3i = ti - vi;
-        xr[c][r0] = sr + ur;
-        xi[c][r0] = si + ui;
-        xr[c][r1] = __fma_rn(p1r, B.x, p1i * B.y);  // * conj(B)
-        xi[c][r1] = __fma_rn(p1i, B.x, -p1r * B.y);
-        xr[c][r2] = __fma_rn(p2r, A.x, p2i * A.y);
-        xi[c][r2] = __fma_rn(p2i, A.x, -p2r * A.y);
-        xr[c][r3] = __fma_rn(p3r, AB.x, p3i * AB.y);
-        xi[c][r3] = __fma_rn(p3i, AB.x, -p3r * AB.y);
+        double *r = xr[c], *i = xi[c];
+        ibfly<false>(r[r0], i[r0], r[r1], i[r1], B.x, B.y);
+        ibfly<true>(r[r2], i[r2], r[r3], i[r3], B.x, B.y);
+        ibfly<false>(r[r0], i[r0], r[r2], i[r2], A.x, A.y);
+        ibfly<false>(r[r1], i[r1], r[r3], i[r3], A.x, A.y);
       }
     }
   }
 
-  // P3: stage 8, pairs (e, e + 4); register bit 1 selects the even-sibling twiddle, bit 0 the factor i
+  // P3: stage 8, pairs (e, e + 4); register bit 1 selects the even sibling's (c, t), bit 0 the factor i
   template <int C>
   __device__ static __forceinline__ void fwd2(double (&xr)[C][E], double (&xi)[C][E], const double2 *tws, int lane,
                                               const double2 *w3 = nullptr) {
-    const double2 W[2] = {w3 ? w3[0] : tws[255 + lane], w3 ? w3[1] : tws[255 + 64 + lane]};
+    const double2 W[2] = {w3 ? w3[0] : tws[TW_P3 + lane], w3 ? w3[1] : tws[TW_P3 + 64 + lane]};
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const double2 w = W[(e >> 1) & 1];
-      const bool odd = e & 1;
+    for (int c = 0; c < C; ++c)
 #pragma unroll
-      for (int c = 0; c < C; ++c) {
-        const double vr = __fma_rn(xr[c][e + 4], w.x, -xi[c][e + 4] * w.y);
-        const double vi = __fma_rn(xr[c][e + 4], w.y, xi[c][e + 4] * w.x);
-        const double ur = xr[c][e], ui = xi[c][e];
-        xr[c][e] = odd ? ur - vi : ur + vr;  // u + i v  |  u + v
-        xi[c][e] = odd ? ui + vr : ui + vi;
-        xr[c][e + 4] = odd ? ur + vi : ur - vr;
-        xi[c][e + 4] = odd ? ui - vr : ui - vi;
+      for (int e = 0; e < 4; ++e) {
+        const double2 w = W[(e >> 1) & 1];
+        if (e & 1)
+          bfly<true>(xr[c][e], xi[c][e], xr[c][e + 4], xi[c][e + 4], w.x, w.y);
+        else
+          bfly<false>(xr[c][e], xi[c][e], xr[c][e + 4], xi[c][e + 4], w.x, w.y);
       }
-    }
   }
   template <int C>
   __device__ static __forceinline__ void inv2(double (&xr)[C][E], double (&xi)[C][E], const double2 *tws, int lane,
                                               const double2 *w3 = nullptr) {
-    const double2 W[2] = {w3 ? w3[0] : tws[255 + lane], w3 ? w3[1] : tws[255 + 64 + lane]};
+    const double2 W[2] = {w3 ? w3[0] : tws[TW_P3 + lane], w3 ? w3[1] : tws[TW_P3 + 64 + lane]};
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const double2 w = W[(e >> 1) & 1];
-      const bool odd = e & 1;
+    for (int c = 0; c < C; ++c)
 #pragma unroll
-      for (int c = 0; c < C; ++c) {
-        const double ur = xr[c][e], ui = xi[c][e];
-        const double dr = ur - xr[c][e + 4], di = ui - xi[c][e + 4];
-        xr[c][e] = ur + xr[c][e + 4];
-        xi[c][e] = ui + xi[c][e + 4];
-        // (dr + i di) * conj(w); odd node: conj(i w) = -i conj(w)
-        const double tr = __fma_rn(dr, w.x, di * w.y), ti = __fma_rn(di, w.x, -dr * w.y);
-        xr[c][e + 4] = odd ? ti : tr;
-        xi[c][e + 4] = odd ? -tr : ti;
+      for (int e = 0; e < 4; ++e) {
+        const double2 w = W[(e >> 1) & 1];
+        if (e & 1)
+          ibfly<true>(xr[c][e], xi[c][e], xr[c][e + 4], xi[c][e + 4], w.x, w.y);
+        else
+          ibfly<false>(xr[c][e], xi[c][e], xr[c][e + 4], xi[c][e + 4], w.x, w.y);
       }
-    }
   }
 
   // C transforms at once (lds holds C * BUF complex)

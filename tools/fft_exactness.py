@@ -262,6 +262,101 @@ class Fft8P(Fft):
         return z
 
 
+class Fft8PT(Fft8P):
+    """The kernel's level-1 transform since round 5 (device_fft.hpp, WgFft): the same passes and
+    layouts as Fft8P, forward butterflies in tangent form (w = c (1 + i t): (p, q) -> (p + c u,
+    p - c u), u = q (1 + i t); a factor i of the node applied to c u), the inverse radix-8 passes
+    premultiplied as in Fft8P, the inverse P1 / P3 butterflies Gentleman-Sande with
+    conj(w) d = c (d (1 - i t))."""
+
+    @staticmethod
+    def _ct(w):
+        c = np.real(w)
+        return c, np.imag(w) / c
+
+    @classmethod
+    def bfly(cls, x, a, b, w, odd):
+        c, t = cls._ct(w)
+        q = x[:, b]
+        u = (q.real - t * q.imag) + 1j * (q.imag + t * q.real)
+        v = c * u * (1j if odd else 1)
+        p = x[:, a].copy()
+        x[:, a], x[:, b] = p + v, p - v
+
+    @classmethod
+    def ibfly(cls, x, a, b, w, odd):
+        c, t = cls._ct(w)
+        d = x[:, a] - x[:, b]
+        x[:, a] = x[:, a] + x[:, b]
+        v = (d.real + t * d.imag) + 1j * (d.imag - t * d.real)
+        x[:, b] = c * v * (-1j if odd else 1)
+
+    def nodes8(self, p):
+        """per-lane A, B, C, w8 C of pass p's radix-8 block"""
+        hi = 0 if p == 0 else self.lane & 31
+        s0 = 0 if p == 0 else 5
+        tw = self.tw
+        return [np.ones(64) * tw[(k << s0) + k * hi + o] for k, o in ((1, 0), (2, 0), (4, 0), (4, 2))]
+
+    def nodes4(self, e0):
+        l = self.lane
+        blk = ((l >> 5) << 2) | (((l >> 4) & 1) << 1) | e0
+        return self.tw[8 + blk], self.tw[16 + 2 * blk]
+
+    def fwd8t(self, x, p):
+        A, B, C, W = self.nodes8(p)
+        for e in range(4):
+            self.bfly(x, e, e + 4, A, False)
+        for a, b, odd in ((0, 2, False), (1, 3, False), (4, 6, True), (5, 7, True)):
+            self.bfly(x, a, b, B, odd)
+        for a, b, w, odd in ((0, 1, C, False), (2, 3, C, True), (4, 5, W, False), (6, 7, W, True)):
+            self.bfly(x, a, b, w, odd)
+
+    def fwd(self, z):
+        x = np.stack([z[self.lane + 64 * e] for e in range(8)], axis=1).astype(np.complex128)
+        self.fwd8t(x, 0)
+        x = self.relayout(x, 0, 1)
+        for e0 in (0, 1):
+            A, B = self.nodes4(e0)
+            r0, r1, r2, r3 = e0, e0 | 2, e0 | 4, e0 | 6
+            self.bfly(x, r0, r2, A, False)
+            self.bfly(x, r1, r3, A, False)
+            self.bfly(x, r0, r1, B, False)
+            self.bfly(x, r2, r3, B, True)
+        x = self.relayout(x, 1, 2)
+        self.fwd8t(x, 2)
+        x = self.relayout(x, 2, 3)
+        W = self.blocks(3)
+        for e in range(4):
+            self.bfly(x, e, e + 4, W[(e >> 1) & 1], bool(e & 1))
+        out = np.zeros(self.n, dtype=np.complex128)
+        for e in range(8):
+            out[self.jidx(3, e)] = x[:, e]
+        return out
+
+    def inv(self, X):
+        x = np.stack([X[self.jidx(3, e)] for e in range(8)], axis=1).astype(np.complex128)
+        W = self.blocks(3)
+        for e in range(4):
+            self.ibfly(x, e, e + 4, W[(e >> 1) & 1], bool(e & 1))
+        x = self.relayout(x, 3, 2)
+        x = self.net8_adj(x) * np.conj(np.stack(self.blocks(2), axis=1))
+        x = self.relayout(x, 2, 1)
+        for e0 in (0, 1):
+            A, B = self.nodes4(e0)
+            r0, r1, r2, r3 = e0, e0 | 2, e0 | 4, e0 | 6
+            self.ibfly(x, r0, r1, B, False)
+            self.ibfly(x, r2, r3, B, True)
+            self.ibfly(x, r0, r2, A, False)
+            self.ibfly(x, r1, r3, A, False)
+        x = self.relayout(x, 1, 0)
+        x = self.net8_adj(x) * np.conj(np.stack(self.blocks(0), axis=1))
+        z = np.zeros(self.n, dtype=np.complex128)
+        for e in range(8):
+            z[self.lane + 64 * e] = x[:, e]
+        return z
+
+
 def fold(p):
     h = len(p) // 2
     return p[:h] + 1j * p[h:]
@@ -291,7 +386,7 @@ def adversarial(keys, dmax, N, rng):
 
 def run(geoms, N, kbits, dmax, rows, trials=4, radix8=False):
     rng = np.random.default_rng(5)
-    ffts = [Fft(*g) for g in geoms] + ([Fft8(*g) for g in geoms] + [Fft8P()] if radix8 else [])
+    ffts = [Fft(*g) for g in geoms] + ([Fft8(*g) for g in geoms] + [Fft8P(), Fft8PT()] if radix8 else [])
     worst = 0.0
     for trial in range(trials):
         keys = [rng.integers(-(1 << (kbits - 1)), 1 << (kbits - 1), N) for _ in range(rows)]
