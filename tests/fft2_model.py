@@ -109,6 +109,28 @@ def fwd_pass(x, p):
     return out
 
 
+def fwd_pass_t(x, p):
+    """fwd_pass in the kernel's tangent form since round 5 (Fft1024::fwd_pass_t): A = c_A (1 + i t_A)
+    on the pairs (0, 2), (1, 3), then B on (0, 1) and i B on (2, 3), each butterfly
+    (p, q) -> (p + c u, p - c u), u = q (1 + i t)."""
+    def bf(y, a, b, w, odd):
+        c, t = w.real, w.imag / w.real
+        q = y[:, b]
+        u = (q.real - t * q.imag) + 1j * (q.imag + t * q.real)
+        v = c * u * (1j if odd else 1)
+        pa = y[:, a].copy()
+        y[:, a], y[:, b] = pa + v, pa - v
+    y = np.array(x, np.complex128)
+    blocks = np.array([tw_index(p, t) for t in range(T)])
+    tw = np.array([block_tw(p, b) for b in range(4 ** p)])  # (B, A, AB) per block
+    B, A = tw[blocks, 0], tw[blocks, 1]
+    bf(y, 0, 2, A, False)
+    bf(y, 1, 3, A, False)
+    bf(y, 0, 1, B, False)
+    bf(y, 2, 3, B, True)
+    return y
+
+
 def inv_pass(x, p):
     """Unscaled inverse of fwd_pass (4 x its inverse)."""
     out = np.empty_like(x)
@@ -208,18 +230,20 @@ def exchange(x, pf, pt):
     return buf[IDX[pt]]
 
 
-def forward(z):
-    """z: complex [1024] natural order -> [256][4] spectrum in the P4 (MAC) layout."""
+def forward(z, tangent=True):
+    """z: complex [1024] natural order -> [256][4] spectrum in the P4 (MAC) layout (tangent: the
+    kernel's forward passes since round 5; False: the premultiplied passes of rounds 3-4)."""
+    fp = fwd_pass_t if tangent else fwd_pass
     x = z[IDX[0]]
-    x = fwd_pass(x, 0)
+    x = fp(x, 0)
     x = relayout_perm(x)
-    x = fwd_pass(x, 1)
+    x = fp(x, 1)
     x = exchange(x, 1, 2)
-    x = fwd_pass(x, 2)
+    x = fp(x, 2)
     x = relayout_perm(x)
-    x = fwd_pass(x, 3)
+    x = fp(x, 3)
     x = exchange(x, 3, 4)
-    return fwd_pass(x, 4)
+    return fp(x, 4)
 
 
 def inverse(X):

@@ -6,7 +6,8 @@ evaluates on the device-stored double-double key spectra at context creation:
       [(delta_fwd + delta_inv + u (1 + 2^-40)) sum_r kappa_{i,r,o} + sqrt(2) u sum_k (2R - 2k) kappa_{i,r(k),o}]
 
 n complex points, R GGSW rows accumulated in the order r(0), r(1), ..., D = sqrt(2n) d_max,
-delta_fwd + delta_inv = 37u + 32u (level 1: tangent-form forward butterflies) or 26u + 26u (level 2), kappa_{i,r,o} = max_j |K_{i,r,o}[j]| (spectrum of key row r of step i, output o;
+delta_fwd + delta_inv = 37u + 32u (level 1) or 41u + 26u (level 2; the forward passes in
+tangent form, DESIGN.md §3a), kappa_{i,r,o} = max_j |K_{i,r,o}[j]| (spectrum of key row r of step i, output o;
 level 2: per 25-bit limb). Spectral magnitudes do not depend on the output order, so a plain
 twisted DFT gives them: K[m] = (1/n) sum_k z_k e^{i pi k / 2n} e^{2 pi i k m / n}."""
 import numpy as np
@@ -42,5 +43,5 @@ def apriori_bounds(dk, q1=134215681, q2=1125899906826241):
     hi = np.rint(r2 / 2.0 ** 25)
     k2 = np.stack([_row_max(r2 - hi * 2.0 ** 25, 1024), _row_max(hi, 1024)], axis=-1).reshape(670, 12, 4)
     e1 = _bound(k1, 512, 8, 16.0, list(range(8)), 37 + 32)
-    e2 = _bound(k2, 1024, 12, 64.0, ORDER2, 26 + 26)
+    e2 = _bound(k2, 1024, 12, 64.0, ORDER2, 41 + 26)
     return e1, e2, float(k1.max()), float(k2.max())

@@ -77,7 +77,7 @@ def test_apriori_bound_proves_both_levels_exact_on_the_bench_key():
     import product_lib as PL
     from fft_bound import apriori_bounds
     e1, e2, k1, k2 = apriori_bounds(PL.keys()[2])
-    assert e1 < 0.15 and e2 < 0.45, (e1, e2)
+    assert e1 < 0.15 and e2 < 0.47, (e1, e2)  # 0.136, 0.445 (round 5: tangent-form forward passes)
     assert 5e6 < k1 < 2e7 and 1e6 < k2 < 3e6  # ~4 sigma of uniform keys' spectra
 
 

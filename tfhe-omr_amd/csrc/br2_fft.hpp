@@ -30,8 +30,12 @@ namespace omr {
 
 struct Fft1024 {
   static constexpr int T = 256, E = 4, n = 1024, L = 10;
-  static constexpr int TW_LEN = 3 * (4 + 16 + 64 + 256);  // passes 1..4: (B, A, AB) per block
+  static constexpr int TW_LEN = 3 * (4 + 16 + 64 + 256);  // passes 1..4: (B, A, AB) per block (inverse)
   OMR_HD static constexpr int tw_off(int p) { return p == 1 ? 0 : p == 2 ? 12 : p == 3 ? 60 : 252; }
+  // the forward passes' tangent forms (cos, tan) of (A, B) per block follow in the global table:
+  // TW_LEN + ct_off(p) + 2 b + k (k: 0 A, 1 B); each thread holds its four blocks' in registers
+  static constexpr int CT_LEN = 2 * (4 + 16 + 64 + 256);
+  OMR_HD static constexpr int ct_off(int p) { return p == 1 ? 0 : p == 2 ? 8 : p == 3 ? 40 : 168; }
 
   // index bit of each position bit (e1, e0, l5, l4, l3, l2, l1, l0, w1, w0), per pass layout
   OMR_HD static constexpr int lay(int p, int k) {
@@ -71,35 +75,19 @@ struct Fft1024 {
   // rotation staging of 2048 real coefficients (doubles): conflict-free ds_write_b64 / ds_read_b64
   OMR_HD static constexpr int slot_stage(int c) { return c ^ (((c >> 6) & 1) << 4); }
 
-  // pass-0 twiddles (block 0): B = w^256 = e^{i pi / 8}, A = w^512 = e^{i pi / 4}, AB = e^{3 i pi / 8}
+  // pass-0 twiddles (block 0): B = w^256 = e^{i pi / 8}, A = w^512 = e^{i pi / 4}, AB = e^{3 i pi / 8};
+  // tangent forms A = R2 (1 + i), B = C8 (1 + i T8)
   static constexpr double C8 = 0.92387953251128675613, S8 = 0.38268343236508977173, R2 = 0.70710678118654752440;
+  static constexpr double T8 = 0.41421356237309504880;  // tan(pi / 8) = sqrt 2 - 1
 
-  __device__ static __forceinline__ void cmul(double &xr, double &xi, double wr, double wi) {
-    const double r = __fma_rn(xr, wr, -xi * wi);
-    const double i = __fma_rn(xr, wi, xi * wr);
-    xr = r;
-    xi = i;
-  }
   __device__ static __forceinline__ void cmulc(double &xr, double &xi, double wr, double wi) {  // * conj(w)
     const double r = __fma_rn(xr, wr, xi * wi);
     const double i = __fma_rn(xi, wr, -xr * wi);
     xr = r;
     xi = i;
   }
-  // radix-4 network after y = T * x: (a0 + a1, a0 - a1, b0 + i b1, b0 - i b1)
-  __device__ static __forceinline__ void net4(double (&xr)[E], double (&xi)[E]) {
-    const double a0r = xr[0] + xr[2], a0i = xi[0] + xi[2], b0r = xr[0] - xr[2], b0i = xi[0] - xi[2];
-    const double a1r = xr[1] + xr[3], a1i = xi[1] + xi[3], b1r = xr[1] - xr[3], b1i = xi[1] - xi[3];
-    xr[0] = a0r + a1r;
-    xi[0] = a0i + a1i;
-    xr[1] = a0r - a1r;
-    xi[1] = a0i - a1i;
-    xr[2] = b0r - b1i;
-    xi[2] = b0i + b1r;
-    xr[3] = b0r + b1i;
-    xi[3] = b0i - b1r;
-  }
-  // adjoint network (4 x its inverse): y0 = a0 + b0, y1 = a1 + b1, y2 = a0 - b0, y3 = a1 - b1
+  // adjoint network of "x *= T = (1, B, A, AB), then (a0 + a1, a0 - a1, b0 + i b1, b0 - i b1)"
+  // (4 x its inverse): y0 = a0 + b0, y1 = a1 + b1, y2 = a0 - b0, y3 = a1 - b1
   __device__ static __forceinline__ void inet4(double (&xr)[E], double (&xi)[E]) {
     const double a0r = xr[0] + xr[1], a0i = xi[0] + xi[1], a1r = xr[0] - xr[1], a1i = xi[0] - xi[1];
     const double b0r = xr[2] + xr[3], b0i = xi[2] + xi[3];
@@ -133,21 +121,6 @@ struct Fft1024 {
       const int r = j - tw_off(P);
       tws[tw_slot(P, r / 3, r % 3)] = twg[j];
     }
-  }
-  template <int P>
-  __device__ static __forceinline__ void fwd_pass(double (&xr)[E], double (&xi)[E], const double2 *tws, int t) {
-    if constexpr (P == 0) {
-      cmul(xr[1], xi[1], C8, S8);
-      cmul(xr[2], xi[2], R2, R2);
-      cmul(xr[3], xi[3], S8, C8);
-    } else {
-      const int b = block<P>(t);
-      const double2 B = tws[tw_slot(P, b, 0)], A = tws[tw_slot(P, b, 1)], AB = tws[tw_slot(P, b, 2)];
-      cmul(xr[1], xi[1], B.x, B.y);
-      cmul(xr[2], xi[2], A.x, A.y);
-      cmul(xr[3], xi[3], AB.x, AB.y);
-    }
-    net4(xr, xi);
   }
   template <int P>
   __device__ static __forceinline__ void inv_pass(double (&xr)[E], double (&xi)[E], const double2 *tws, int t) {
@@ -216,52 +189,48 @@ struct Fft1024 {
     __builtin_amdgcn_wave_barrier();  // the next writes stay below these reads (in-order LDS per wave)
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
   }
-  // passes with the block's twiddles (B, A, AB) already in registers
-  __device__ static __forceinline__ void fwd_pass_r(double (&xr)[E], double (&xi)[E], const double2 (&w)[3]) {
-    cmul(xr[1], xi[1], w[0].x, w[0].y);
-    cmul(xr[2], xi[2], w[1].x, w[1].y);
-    cmul(xr[3], xi[3], w[2].x, w[2].y);
-    net4(xr, xi);
+  // forward radix-4 pass in tangent form (device_fft.hpp, bfly): the tree's stage A on the pairs
+  // (0, 2), (1, 3), then B on (0, 1) and i B on (2, 3) -- the same map as "T = (1, B, A, AB), then
+  // net4" in 24 FMAs instead of 28 operations
+  __device__ static __forceinline__ void fwd_pass_t(double (&xr)[E], double (&xi)[E], double2 A, double2 B) {
+    bfly<false>(xr[0], xi[0], xr[2], xi[2], A.x, A.y);
+    bfly<false>(xr[1], xi[1], xr[3], xi[3], A.x, A.y);
+    bfly<false>(xr[0], xi[0], xr[1], xi[1], B.x, B.y);
+    bfly<true>(xr[2], xi[2], xr[3], xi[3], B.x, B.y);
   }
-  __device__ static __forceinline__ void inv_pass_r(double (&xr)[E], double (&xi)[E], const double2 (&w)[3]) {
-    inet4(xr, xi);
-    cmulc(xr[1], xi[1], w[0].x, w[0].y);
-    cmulc(xr[2], xi[2], w[1].x, w[1].y);
-    cmulc(xr[3], xi[3], w[2].x, w[2].y);
-  }
-  // thread t's twiddles of pass P (its block is the same for all four registers and all transforms)
+  // thread t's (A, B) tangent forms of pass P from the global table (its block is the same for all
+  // four registers and all transforms)
   template <int P>
-  __device__ static __forceinline__ void block_twiddles(double2 (&w)[3], const double2 *tws, int t) {
+  __device__ static __forceinline__ void block_ct(double2 (&w)[2], const double2 *__restrict__ twg, int t) {
     const int b = block<P>(t);
 #pragma unroll
-    for (int k = 0; k < 3; ++k) w[k] = tws[tw_slot(P, b, k)];
+    for (int k = 0; k < 2; ++k) w[k] = twg[TW_LEN + ct_off(P) + 2 * b + k];
   }
   // forward: in P0 layout (point idx(0, t, e)), out P4 layout. X: this transform's cross-wave buffer;
   // the wave-local exchange (P3 -> P4) runs in the wave's own quarter of X (slot bits 9, 8 = wave:
   // tests/test_fft2_layout.py::test_exchange_regions), which after this transform's cross-wave reads
-  // no other wave touches until the next-but-one transform writes X behind the next barrier. Passes
-  // 3 and 4 on the thread's twiddles held in registers (w3, w4: block_twiddles<3>, <4>).
-  __device__ static __forceinline__ void fwd(double (&xr)[E], double (&xi)[E], double2 *X, const double2 *tws, int t,
-                                             const double2 (&w3)[3], const double2 (&w4)[3]) {
-    fwd_pass<0>(xr, xi, tws, t);
+  // no other wave touches until the next-but-one transform writes X behind the next barrier. Every
+  // pass in tangent form on the thread's (A, B) held in registers (wc[P - 1]: block_ct<P>).
+  __device__ static __forceinline__ void fwd(double (&xr)[E], double (&xi)[E], double2 *X, int t,
+                                             const double2 (&wc)[4][2]) {
+    fwd_pass_t(xr, xi, make_double2(R2, 1.0), make_double2(C8, T8));
     perm(xr, xi);
-    fwd_pass<1>(xr, xi, tws, t);
+    fwd_pass_t(xr, xi, wc[0][0], wc[0][1]);
     exchange<1, 2, 0, true>(xr, xi, X, t);
-    fwd_pass<2>(xr, xi, tws, t);
+    fwd_pass_t(xr, xi, wc[1][0], wc[1][1]);
     perm(xr, xi);
-    fwd_pass_r(xr, xi, w3);
+    fwd_pass_t(xr, xi, wc[2][0], wc[2][1]);
     exchange<3, 4, 2, false>(xr, xi, X, t);
-    fwd_pass_r(xr, xi, w4);
+    fwd_pass_t(xr, xi, wc[3][0], wc[3][1]);
   }
   // unscaled inverse (x 1024; the keys carry 1/1024): in P4 layout, out P0 layout; the wave-local
   // exchange first, in the wave's own quarter of X (which the previous use of X, two cross-wave
   // uses back, has finished with behind the last barrier), then the cross-wave one (own-quarter
   // writes)
-  __device__ static __forceinline__ void inv(double (&xr)[E], double (&xi)[E], double2 *X, const double2 *tws, int t,
-                                             const double2 (&w3)[3], const double2 (&w4)[3]) {
-    inv_pass_r(xr, xi, w4);
+  __device__ static __forceinline__ void inv(double (&xr)[E], double (&xi)[E], double2 *X, const double2 *tws, int t) {
+    inv_pass<4>(xr, xi, tws, t);
     exchange<4, 3, 3, false>(xr, xi, X, t);
-    inv_pass_r(xr, xi, w3);
+    inv_pass<3>(xr, xi, tws, t);
     perm(xr, xi);
     inv_pass<2>(xr, xi, tws, t);
     exchange<2, 1, 1, true>(xr, xi, X, t);
@@ -362,8 +331,7 @@ template <int W>
 __device__ __forceinline__ void br2f_digit(const uint32_t (&pk)[2][Fft1024::E][Digits2S::DW], int j, int q, int nx,
                                            double (&sr)[2][2][Fft1024::E], double (&si)[2][2][Fft1024::E],
                                            double2 (&ka)[2][Fft1024::E], double2 (&kb)[2][Fft1024::E], double2 *X,
-                                           const double2 *tws, __amdgpu_buffer_rsrc_t rsrc, uint32_t t16, int t,
-                                           const double2 (&w3)[3], const double2 (&w4)[3]) {
+                                           __amdgpu_buffer_rsrc_t rsrc, uint32_t t16, int t, const double2 (&wc)[4][2]) {
   using F = Fft1024;
   constexpr int E = F::E;
   double xr[E], xi[E];
@@ -372,7 +340,7 @@ __device__ __forceinline__ void br2f_digit(const uint32_t (&pk)[2][Fft1024::E][D
     xr[e] = Digits2S::digit<W>(pk[0][e], j);
     xi[e] = Digits2S::digit<W>(pk[1][e], j);
   }
-  F::fwd(xr, xi, X, tws, t, w3, w4);
+  F::fwd(xr, xi, X, t, wc);
   br2f_load_half(kb, rsrc, q, 1, t16);
 #pragma unroll
   for (int o = 0; o < 2; ++o) {
@@ -414,7 +382,8 @@ __device__ __forceinline__ void br2f_update(double *aco, const double (&sr)[2][F
 // hom_trace (detector.rs:626-639), the NttRlweCiphertext (mode 0).
 // The accumulator lives in LDS (ACC_p at slot_stage positions): each step reads the rotated digits
 // of ACC_p straight from it and the update writes it in place, so there is no staging exchange and
-// its 32 VGPRs hold the thread's pass-3 / pass-4 twiddles instead (round 5). Per CMUX step: for
+// its 32 VGPRs hold the thread's forward twiddles instead (round 5: the tangent forms of passes
+// 1..4, the inverse reading the premultiplied (B, A, AB) from LDS). Per CMUX step: for
 // each of the 12 digits in issue order (poly p, digit j + 3 w) a forward transform and the
 // multiply-accumulate into the four (output, limb) spectra with the key row (output A's blocks
 // loaded one digit ahead); then the four inverses, rounding, limb recombination mod q2 and the
@@ -452,9 +421,11 @@ __device__ __forceinline__ void br2f_body(const uint32_t *__restrict__ lwe_int, 
       }
   }
   __syncthreads();
-  double2 w3[3], w4[3];  // this thread's pass-3 / pass-4 twiddles, for every transform of the rotation
-  F::block_twiddles<3>(w3, tws, t);
-  F::block_twiddles<4>(w4, tws, t);
+  double2 wc[4][2];  // this thread's forward twiddles of passes 1..4, for every transform of the rotation
+  F::block_ct<1>(wc[0], twg, t);
+  F::block_ct<2>(wc[1], twg, t);
+  F::block_ct<3>(wc[2], twg, t);
+  F::block_ct<4>(wc[3], twg, t);
   double2 ka[2][E], kb[2][E];
   const __amdgpu_buffer_rsrc_t rsrc = bsk2_rsrc(bskf);
   const uint32_t t16 = (uint32_t)t * 16u;
@@ -488,15 +459,15 @@ __device__ __forceinline__ void br2f_body(const uint32_t *__restrict__ lwe_int, 
       }
 #pragma unroll 1
       for (int j = 0; j < D2 / 2; ++j) {
-        br2f_digit<0>(pk, j, q0 + p * D2 + j, nxt(j, 0), sr, si, ka, kb, Xb[0], tws, rsrc, t16, t, w3, w4);
-        br2f_digit<1>(pk, j, q0 + p * D2 + j + 3, nxt(j, 1), sr, si, ka, kb, Xb[1], tws, rsrc, t16, t, w3, w4);
+        br2f_digit<0>(pk, j, q0 + p * D2 + j, nxt(j, 0), sr, si, ka, kb, Xb[0], rsrc, t16, t, wc);
+        br2f_digit<1>(pk, j, q0 + p * D2 + j + 3, nxt(j, 1), sr, si, ka, kb, Xb[1], rsrc, t16, t, wc);
       }
     }
     // inverses on X0, X1, X0, X1, rounding to the exact limb products, recombination mod q2
 #pragma unroll
     for (int o = 0; o < 2; ++o) {
 #pragma unroll
-      for (int l = 0; l < 2; ++l) F::inv(sr[o][l], si[o][l], Xb[l], tws, t, w3, w4);
+      for (int l = 0; l < 2; ++l) F::inv(sr[o][l], si[o][l], Xb[l], tws, t);
       br2f_update<G>(acs + o * NN, sr[o], si[o], rg, t);
     }
   }

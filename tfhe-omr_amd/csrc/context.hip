@@ -135,7 +135,8 @@ std::vector<double2> fft_twiddles() {
   return tw;
 }
 
-// Fft1024 twiddles (br2_fft.hpp): pass p = 1..4, block hi -> (B, A, AB) at tw_off(p) + 3 hi, with
+// Fft1024 twiddles (br2_fft.hpp): pass p = 1..4, block hi -> (B, A, AB) at tw_off(p) + 3 hi (the
+// inverse), then the forward's tangent forms (cos, tan) of (A, B) at TW_LEN + ct_off(p) + 2 hi, with
 // A = W(2p, hi), B = W(2p + 1, 2 hi) of the tree with n = 1024 (eps(0, 0) = n, w = e^{i pi / 2n});
 // each entry an exact angle evaluated in long double and rounded once.
 std::vector<double2> fft2_twiddles() {
@@ -155,7 +156,12 @@ std::vector<double2> fft2_twiddles() {
     const long double ang = 3.14159265358979323846264338327950288L * (long double)(h % (8 * n)) / (long double)(2 * n);
     return make_double2((double)cosl(ang), (double)sinl(ang));
   };
-  std::vector<double2> tw(Fft1024::TW_LEN);
+  auto ct = [&](long h) {  // tangent form (cos, tan); no node of the tree lies on an axis
+    const long double ang = 3.14159265358979323846264338327950288L * (long double)(h % (8 * n)) / (long double)(2 * n);
+    const long double c = cosl(ang), s = sinl(ang);
+    return make_double2((double)c, (double)(s / c));
+  };
+  std::vector<double2> tw(Fft1024::TW_LEN + Fft1024::CT_LEN);
   int off = 0;
   for (int p = 1; p <= 4; ++p)
     for (int hi = 0; hi < (1 << (2 * p)); ++hi) {
@@ -163,6 +169,8 @@ std::vector<double2> fft2_twiddles() {
       tw[off++] = at(b);
       tw[off++] = at(a);
       tw[off++] = at(a + b);
+      tw[Fft1024::TW_LEN + Fft1024::ct_off(p) + 2 * hi] = ct(a);
+      tw[Fft1024::TW_LEN + Fft1024::ct_off(p) + 2 * hi + 1] = ct(b);
     }
   return tw;
 }
@@ -225,9 +233,9 @@ std::vector<CDD> dd_tree_twiddles(int L) {
 // (row_max_abs_kernel), the rows accumulated in the order r(0), r(1), ... by two fmas each:
 //   E = n D (1 + 2^-30) [(delta_fwd + delta_inv + u (1 + 2^-40)) sum_r kappa_r + sqrt(2) u sum_k (2R - 2k) kappa_r(k)]
 // the forward digit transforms within delta_fwd and the inverse within delta_inv relative 2-norm
-// error (level 2, premultiplied radix-4 passes: 26u each; level 1: 37u forward -- 4u per
-// tangent-form radix-2 stage, 9 stages -- and 32u inverse -- 8u per premultiplied radix-8 pass,
-// 5u per Gentleman-Sande stage of P1 and P3 -- rounded up), the sequential fma accumulation, and
+// error (forward in tangent form, 4u per radix-2 stage: level 1 37u (9 stages), level 2 41u (10);
+// inverse: level 1 32u -- 8u per premultiplied radix-8 pass, 5u per Gentleman-Sande stage of P1 and
+// P3 --, level 2 26u -- 5u per premultiplied radix-4 pass --, rounded up), the sequential fma accumulation, and
 // the double-double keys' |K^ - K| <= u |K|. The maximum over every step and output spectrum.
 // kmax: [steps][rows][outputs] (level 1: [512][8][2]; level 2: [670][12][2 out][2 limb], the limbs
 // as two more "outputs").
@@ -239,7 +247,7 @@ double apriori_bound(int level, const std::vector<double> &kmax) {
   // g = 2 j + w, row p D2 + j + 3 w (br2_fft.hpp)
   const int order2[12] = {0, 3, 1, 4, 2, 5, 6, 9, 7, 10, 8, 11};
   const double D = std::sqrt(2.0 * n) * (level == 1 ? 16.0 : 64.0);
-  const double dft = level == 1 ? 37 + 32 : 26 + 26;  // delta_fwd + delta_inv, in units of u
+  const double dft = level == 1 ? 37 + 32 : 41 + 26;  // delta_fwd + delta_inv, in units of u
   const double cf = dft * u + u * (1 + 0x1p-40), cw = std::sqrt(2.0) * u;
   double worst = 0.0;
   for (int i = 0; i < steps; ++i)

@@ -38,6 +38,40 @@ __device__ __forceinline__ void wave_lds_fence() {
   __builtin_amdgcn_wave_barrier();
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
 }
+// forward radix-2 butterfly in tangent form: (p, q) <- (p + w q, p - w q), w = c (1 + i t);
+// I: the node's twiddle is i w
+template <bool I>
+__device__ __forceinline__ void bfly(double &pr, double &pi, double &qr, double &qi, double c, double t) {
+  const double ur = __fma_rn(-t, qi, qr), ui = __fma_rn(t, qr, qi);  // u = q (1 + i t), w q = c u
+  const double ar = pr, ai = pi;
+  if constexpr (!I) {
+    pr = __fma_rn(c, ur, ar);
+    pi = __fma_rn(c, ui, ai);
+    qr = __fma_rn(-c, ur, ar);
+    qi = __fma_rn(-c, ui, ai);
+  } else {  // i c u = c (-ui + i ur)
+    pr = __fma_rn(-c, ui, ar);
+    pi = __fma_rn(c, ur, ai);
+    qr = __fma_rn(c, ui, ar);
+    qi = __fma_rn(-c, ur, ai);
+  }
+}
+// its unscaled inverse (Gentleman-Sande): (p, q) <- (p + q, conj(w) (p - q)); conj(i w) = -i conj(w)
+template <bool I>
+__device__ __forceinline__ void ibfly(double &pr, double &pi, double &qr, double &qi, double c, double t) {
+  const double dr = pr - qr, di = pi - qi;
+  pr = pr + qr;
+  pi = pi + qi;
+  const double vr = __fma_rn(t, di, dr), vi = __fma_rn(-t, dr, di);  // v = d (1 - i t), conj(w) d = c v
+  if constexpr (!I) {
+    qr = c * vr;
+    qi = c * vi;
+  } else {  // -i c v = c (vi - i vr)
+    qr = c * vi;
+    qi = -c * vr;
+  }
+}
+
 // Level-1 transform: 512 complex points, one wave (64 lanes x 8 registers), index bits j8..j0
 // (stage s splits on bit 8 - s). Four passes of 3, 2, 3 and 1 stages; jidx(p, lane, e) is the
 // index register e of `lane` holds in pass p:
@@ -162,40 +196,6 @@ struct WgFft {
                                                 int lane) {
     if constexpr (P == 0) return G ? gtw[TW_P0F + k] : tws[TW_P0F + k];
     return tws[TW_P2F + k * 32 + (lane & 31)];
-  }
-
-  // forward radix-2 butterfly in tangent form: (p, q) <- (p + w q, p - w q), w = c (1 + i t);
-  // I: the node's twiddle is i w
-  template <bool I>
-  __device__ static __forceinline__ void bfly(double &pr, double &pi, double &qr, double &qi, double c, double t) {
-    const double ur = __fma_rn(-t, qi, qr), ui = __fma_rn(t, qr, qi);  // u = q (1 + i t), w q = c u
-    const double ar = pr, ai = pi;
-    if constexpr (!I) {
-      pr = __fma_rn(c, ur, ar);
-      pi = __fma_rn(c, ui, ai);
-      qr = __fma_rn(-c, ur, ar);
-      qi = __fma_rn(-c, ui, ai);
-    } else {  // i c u = c (-ui + i ur)
-      pr = __fma_rn(-c, ui, ar);
-      pi = __fma_rn(c, ur, ai);
-      qr = __fma_rn(c, ui, ar);
-      qi = __fma_rn(-c, ur, ai);
-    }
-  }
-  // its unscaled inverse (Gentleman-Sande): (p, q) <- (p + q, conj(w) (p - q)); conj(i w) = -i conj(w)
-  template <bool I>
-  __device__ static __forceinline__ void ibfly(double &pr, double &pi, double &qr, double &qi, double c, double t) {
-    const double dr = pr - qr, di = pi - qi;
-    pr = pr + qr;
-    pi = pi + qi;
-    const double vr = __fma_rn(t, di, dr), vi = __fma_rn(-t, dr, di);  // v = d (1 - i t), conj(w) d = c v
-    if constexpr (!I) {
-      qr = c * vr;
-      qi = c * vi;
-    } else {  // -i c v = c (vi - i vr)
-      qr = c * vi;
-      qi = -c * vr;
-    }
   }
 
   template <int P, int C, bool G = false>
