@@ -27,10 +27,11 @@ def _row_max(rows, n):
     return np.abs(np.fft.fft(z * tw, axis=-1)).max(axis=-1) / n
 
 
-def _bound(kmax, n, R, dmax, order, dft):
-    """kmax [steps][R][outputs]; dft = (delta_fwd + delta_inv) / u"""
+def _bound(kmax, n, R, dmax, order, dft, weights=None):
+    """kmax [steps][R][outputs]; dft = (delta_fwd + delta_inv) / u; weights: the MAC's rounding
+    weight per position of `order` (default: one chain of 2R fmas, 2R - 2k)"""
     k = kmax[:, order, :]
-    w = (2.0 * R - 2.0 * np.arange(R))[None, :, None]
+    w = (2.0 * R - 2.0 * np.arange(R) if weights is None else np.asarray(weights, np.float64))[None, :, None]
     inner = (dft * U + U * (1 + 2.0 ** -40)) * k.sum(axis=1) + np.sqrt(2.0) * U * (w * k).sum(axis=1)
     return n * np.sqrt(2.0 * n) * dmax * inner.max() * (1 + 2.0 ** -30)
 
@@ -45,3 +46,13 @@ def apriori_bounds(dk, q1=134215681, q2=1125899906826241):
     e1 = _bound(k1, 512, 8, 16.0, list(range(8)), 37 + 32)
     e2 = _bound(k2, 1024, 12, 64.0, ORDER2, 41 + 26)
     return e1, e2, float(k1.max()), float(k2.max())
+
+
+def apriori_bound_latency2(dk, q2=1125899906826241):
+    """Level 2 as br2y_kernel (the latency path) accumulates it (context.hip, apriori_bound level 3):
+    each group chains its three rows (weights 6, 4, 2), then two additions: 8 - 2 j for digit
+    3 g + j of either polynomial."""
+    r2 = _centred(dk.bsk2.reshape(670, 12, 2, 2048), q2)
+    hi = np.rint(r2 / 2.0 ** 25)
+    k2 = np.stack([_row_max(r2 - hi * 2.0 ** 25, 1024), _row_max(hi, 1024)], axis=-1).reshape(670, 12, 4)
+    return _bound(k2, 1024, 12, 64.0, list(range(12)), 41 + 26, [8 - 2 * ((r % 6) % 3) for r in range(12)])

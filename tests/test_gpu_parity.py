@@ -166,6 +166,29 @@ def test_latency_level2_variants_match_throughput(real):
             assert (dec[0] == 1) == mask[m] and not dec[1:].any()
 
 
+def test_latency_level2_fft_two_cu_matches_ntt(real, monkeypatch):
+    """The latency path's level 2 on the FFT over two CUs per message (br2y_kernel: a context
+    created with OMR_BR2Y=1; it runs when the a priori bound of its accumulation order is below
+    0.5) against the default exact modular-NTT two-CU kernel (br2x_kernel) on the same level-1
+    outputs, bit for bit, rotation and rotation + trace, at 1, 7 and 64 messages (2, 14 and 128
+    CUs)."""
+    _, ntt, _ = real
+    _, _, dk = PL.keys()
+    monkeypatch.setenv("OMR_BR2Y", "1")
+    det = A.Detector(dk)
+    monkeypatch.delenv("OMR_BR2Y")
+    try:
+        for n in (1, 7, 64):
+            mask = np.zeros(n, dtype=bool)
+            mask[::5] = True
+            ca, cb = PL.mixed_clues(mask, seed=1200 + n)
+            fl = det.first_level(ca, cb)
+            assert np.array_equal(det.blind_rotate_level2(fl), ntt.blind_rotate_level2(fl)), n
+            assert np.array_equal(det.second_level(fl), ntt.second_level(fl)), n
+    finally:
+        det.close()
+
+
 def test_level2_throughput_small_batches(real):
     """The throughput level-2 kernel (br2f_kernel, FFT) at batches of 5 and 6 messages against the
     latency kernels (the oracle-checked NTT path), rotation and rotation + trace."""

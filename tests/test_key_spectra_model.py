@@ -79,6 +79,9 @@ def test_apriori_bound_proves_both_levels_exact_on_the_bench_key():
     e1, e2, k1, k2 = apriori_bounds(PL.keys()[2])
     assert e1 < 0.15 and e2 < 0.47, (e1, e2)  # 0.136, 0.445 (round 5: tangent-form forward passes)
     assert 5e6 < k1 < 2e7 and 1e6 < k2 < 3e6  # ~4 sigma of uniform keys' spectra
+    from fft_bound import apriori_bound_latency2
+    ey = apriori_bound_latency2(PL.keys()[2])
+    assert ey < e2, (ey, e2)  # the latency path's shorter chains (br2y_kernel) round less
 
 
 def test_double_double_twiddles_match_long_double():

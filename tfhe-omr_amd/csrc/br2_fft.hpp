@@ -519,4 +519,232 @@ __global__ __launch_bounds__(256, 2) void br2f_guard_kernel(const uint32_t *__re
   br2f_body<true>(lwe_int, bskf, twg, tk, tb, out, mode, margin);
 }
 
+
+// ---- level 2 over two CUs per message on the exact FFT (the latency path) --------------------
+// br2x_kernel's division of labour (latency_kernels.hpp) on br2f's arithmetic. Workgroup 2m + r
+// owns polynomial r (0 mask, 1 body) of message m and its accumulator ACC_r (LDS, slot_stage
+// positions). Its group g (256 threads: one Fft1024 transform) takes word g of the Digits2S
+// decomposition of (X^a - 1) ACC_r -- digits 3g + j, GGSW rows r D2 + 3g + j -- and for each digit
+// runs the forward transform and multiply-accumulates the four (output, limb) spectra. Group g
+// finalises limb g of output r: the groups swap their limb-(1 - g) partials of both outputs through
+// LDS; group g keeps limb g of output r and sends limb g of output 1 - r to the partner workgroup
+// through global memory under br2x's hand-off rules (sc1 stores, vmcnt(0), a barrier, one flag
+// carrying the executed-step count, a bounded poll, sc1 loads; slot = step parity); it adds the
+// partner's limb g of output r, runs the inverse, rounds, and the groups swap half of the rounded
+// limbs so that each recombines (mod q2) and updates 1,024 of ACC_r's coefficients. Per CU and
+// step: three forward transforms per group, one inverse, one hand-off -- br2x's schedule, with
+// transforms of 120 / 140 FP64 operations per thread instead of the modular NTT's ~450.
+// Key rows: output A's two limb blocks of the next digit are issued after output A's MAC, output
+// B's after output B's (in flight across the next transform); the next step's first row is issued
+// once the partner's payload has been consumed, so no wait of the hand-off covers it and it stays
+// in flight across the inverse, the update and the next step's digit extraction.
+// Exact when the a priori bound of this accumulation order (apriori_bound level 3) is below 0.5;
+// otherwise, or on a guarded context, the host runs br2x_kernel's exact NTT instead.
+// LDS: twiddles 16 KB, X0 / X1 of each group 64 KB, the limb swap 32 KB (+ the groups' X1), ACC_r
+// 16 KB: 128 KB, one workgroup per CU.
+constexpr int BR2Y_T = 2 * Fft1024::T;
+
+__global__ __launch_bounds__(BR2Y_T, 1) void br2y_kernel(const uint32_t *__restrict__ lwe_int,
+                                                         const double2 *__restrict__ bskf,
+                                                         const double2 *__restrict__ twg, DeviceTables tb,
+                                                         double *xg, uint32_t *flags, int *err,
+                                                         uint64_t *__restrict__ out) {
+  using F = Fft1024;
+  using M = Mod<2>;
+  constexpr int E = F::E, NN = N2, n = F::n, T = F::T;
+  __shared__ double2 tws[n];
+  __shared__ double2 xb[2][2][n];  // [group][X0, X1]
+  __shared__ double2 px[2][n];     // [group]: its limb-(1 - g) partial of output 1 - r; the rounded halves
+  __shared__ double acs[NN];       // ACC_r
+  __shared__ int stop;
+  const int m = blockIdx.x >> 1, r = blockIdx.x & 1;
+  const int g = __builtin_amdgcn_readfirstlane((int)threadIdx.x / T), t = (int)threadIdx.x % T;
+  const uint32_t *lwe = lwe_int + (size_t)m * (NI + 1);
+  if (g == 0) F::load_twiddles(tws, twg, t);
+  {  // ACC_r = X^{-b} * LUT2 (body) or 0 (mask)
+    const int b = (int)lwe[NI];
+    const int rr = (2 * NN - (b % (2 * NN))) % (2 * NN);
+    for (int c = (int)threadIdx.x; c < NN; c += BR2Y_T)
+      acs[F::slot_stage(c)] = r == 1 ? canon_small<M>(rot_read<NN>(tb.lut2, c, rr)) : 0.0;
+    if (threadIdx.x == 0) stop = 0;
+  }
+  double2 wc[4][2];  // this thread's forward twiddles of passes 1..4
+  F::block_ct<1>(wc[0], twg, t);
+  F::block_ct<2>(wc[1], twg, t);
+  F::block_ct<3>(wc[2], twg, t);
+  F::block_ct<4>(wc[3], twg, t);
+  const __amdgpu_buffer_rsrc_t rsrc = bsk2_rsrc(bskf);
+  const uint32_t t16 = (uint32_t)t * 16u;
+  uint32_t *my_flag = flags + 2 * m + r, *their_flag = flags + 2 * m + (1 - r);
+  uint32_t hc = 0;  // hand-offs so far (executed steps)
+  double2 ka[2][E], kb[2][E];
+  int pre = -1;  // the step whose first row ka / kb hold
+#pragma unroll 1
+  for (int i = 0; i < NI; ++i) {
+    const int a = (int)__builtin_amdgcn_readfirstlane(lwe[i]) & (2 * NN - 1);
+    if (a == 0) continue;  // (X^0 - 1) * ACC = 0 (both workgroups of the message skip it)
+    const int q0 = i * 2 * D2 + r * D2 + 3 * g;  // the group's first GGSW row of this step
+#ifdef OMR_BR2Y_NOKEY
+#define br2y_load(...) ((void)0)
+    if (i == 0 || pre == -1) {
+      br2f_load_half(ka, rsrc, q0, 0, t16);
+      br2f_load_half(kb, rsrc, q0, 1, t16);
+      pre = -2;
+    }
+#else
+#define br2y_load(...) br2f_load_half(__VA_ARGS__)
+    if (pre != i) {
+      br2f_load_half(ka, rsrc, q0, 0, t16);
+      br2f_load_half(kb, rsrc, q0, 1, t16);
+    }
+#endif
+    wg_barrier_lds();  // ACC_r (init or the previous update) visible; the previous step's LDS reads done
+    uint32_t pw[2][E];  // word g of the digits at the thread's P0 points (coefficients j, j + 1024)
+    {
+      uint32_t pk[2][E][Digits2S::DW];
+      br2f_digits(acs, a, t, pk);
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int e = 0; e < E; ++e) pw[h][e] = g ? pk[h][e][1] : pk[h][e][0];
+    }
+    double sr[2][2][E], si[2][2][E];  // [output][limb] partial spectra of the group's three digits
+#pragma unroll
+    for (int o = 0; o < 2; ++o)
+#pragma unroll
+      for (int l = 0; l < 2; ++l)
+#pragma unroll
+        for (int e = 0; e < E; ++e) sr[o][l][e] = si[o][l][e] = 0.0;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int wd = g == 1 && j == 2 ? 18 : 7;  // the top digit of word 1 is its sign-extended rest
+      double xr[E], xi[E];
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        xr[e] = (double)(int)__builtin_amdgcn_sbfe(pw[0][e], 7 * j, wd);
+        xi[e] = (double)(int)__builtin_amdgcn_sbfe(pw[1][e], 7 * j, wd);
+      }
+      F::fwd(xr, xi, xb[g][j & 1], t, wc);
+#pragma unroll
+      for (int o = 0; o < 2; ++o) {
+#pragma unroll
+        for (int l = 0; l < 2; ++l)
+#pragma unroll
+          for (int e = 0; e < E; ++e) {
+            const double2 kv = o ? kb[l][e] : ka[l][e];
+            sr[o][l][e] = __fma_rn(xr[e], kv.x, __fma_rn(-xi[e], kv.y, sr[o][l][e]));
+            si[o][l][e] = __fma_rn(xr[e], kv.y, __fma_rn(xi[e], kv.x, si[o][l][e]));
+          }
+        if (j < 2) {
+          if (o == 0)
+            br2y_load(ka, rsrc, q0 + j + 1, 0, t16);
+          else
+            br2y_load(kb, rsrc, q0 + j + 1, 1, t16);
+        }
+      }
+    }
+    // the four partials by role (r and g are uniform: selects, no dynamic register indexing):
+    // [0] output r limb g (kept), [1] output r limb 1 - g, [2] output 1 - r limb g (handed to the
+    // partner), [3] output 1 - r limb 1 - g
+    double pr4[4][E], pi4[4][E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const double rlr = r ? sr[1][0][e] : sr[0][0][e], rhr = r ? sr[1][1][e] : sr[0][1][e];
+      const double nlr = r ? sr[0][0][e] : sr[1][0][e], nhr = r ? sr[0][1][e] : sr[1][1][e];
+      const double rli = r ? si[1][0][e] : si[0][0][e], rhi = r ? si[1][1][e] : si[0][1][e];
+      const double nli = r ? si[0][0][e] : si[1][0][e], nhi = r ? si[0][1][e] : si[1][1][e];
+      pr4[0][e] = g ? rhr : rlr;
+      pi4[0][e] = g ? rhi : rli;
+      pr4[1][e] = g ? rlr : rhr;
+      pi4[1][e] = g ? rli : rhi;
+      pr4[2][e] = g ? nhr : nlr;
+      pi4[2][e] = g ? nhi : nli;
+      pr4[3][e] = g ? nlr : nhr;
+      pi4[3][e] = g ? nli : nhi;
+    }
+    // limb swap: group g posts its limb-(1 - g) partials (output r in its X1, free since the third
+    // transform's barrier; output 1 - r in px[g]) and takes the other group's limb-g ones
+    {
+      double2 *pr_ = xb[g][1], *ph = px[g];
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        pr_[e * T + t] = make_double2(pr4[1][e], pi4[1][e]);
+        ph[e * T + t] = make_double2(pr4[3][e], pi4[3][e]);
+      }
+    }
+    wg_barrier_lds();
+    double fr[E], fi[E];  // limb g of output r: this workgroup's six rows, then the partner's six
+    {
+      const double2 *qr = xb[1 - g][1], *qh = px[1 - g];
+      const size_t slot = hc & 1;
+      double *dst = xg + ((((size_t)m * 2 + r) * 2 + slot) * 2 + g) * 2 * n;
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const double2 vr = qr[e * T + t], vh = qh[e * T + t];
+        fr[e] = pr4[0][e] + vr.x;
+        fi[e] = pi4[0][e] + vr.y;
+        st_sc1(dst + e * T + t, pr4[2][e] + vh.x);  // limb g of output 1 - r: the partner's
+        st_sc1(dst + n + e * T + t, pi4[2][e] + vh.y);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __hip_atomic_store(my_flag, hc + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      int k = 0;
+      while (__hip_atomic_load(their_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < hc + 1) {
+        if (++k == BR2X_SPIN) {
+          stop = 1;
+          atomicExch(err, 1);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+    }
+    __syncthreads();
+    if (stop) break;
+    {  // the partner's limb g of output r
+      const double *src = xg + ((((size_t)m * 2 + (1 - r)) * 2 + (hc & 1)) * 2 + g) * 2 * n;
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        fr[e] += ld_sc1(src + e * T + t);
+        fi[e] += ld_sc1(src + n + e * T + t);
+      }
+    }
+    asm volatile("" : "+v"(fr[0]), "+v"(fr[1]), "+v"(fr[2]), "+v"(fr[3]), "+v"(fi[0]), "+v"(fi[1]), "+v"(fi[2]),
+                 "+v"(fi[3])::"memory");  // consumed before the prefetch below is issued
+#ifndef OMR_BR2Y_NOKEY
+    if (i + 1 < NI) {  // the next step's first row (kept when that step runs next)
+      br2f_load_half(ka, rsrc, q0 + 2 * D2, 0, t16);
+      br2f_load_half(kb, rsrc, q0 + 2 * D2, 1, t16);
+      pre = i + 1;
+    }
+#endif
+    F::inv(fr, fi, xb[g][1], tws, t);  // X1: every reader of the limb swap passed the hand-off barriers
+    // round limb g; the groups swap halves: group g recombines the coefficients idx(0, t, e) + 1024 g
+    double lv[2][E];  // [h][e]: limb g of coefficient idx(0, t, e) + 1024 h
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      lv[0][e] = rint(fr[e]);
+      lv[1][e] = rint(fi[e]);
+    }
+    double *hx = reinterpret_cast<double *>(px[g]);
+#pragma unroll
+    for (int e = 0; e < E; ++e) hx[e * T + t] = g ? lv[0][e] : lv[1][e];
+    wg_barrier_lds();
+    const double *ho = reinterpret_cast<const double *>(px[1 - g]);
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const double other = ho[e * T + t];
+      const double lo = g == 0 ? lv[0][e] : other, hr = g == 0 ? other : lv[1][e];
+      double &acc = acs[F::slot_stage(F::idx(0, t, e) + n * g)];
+      acc = canon<M>(acc + red<M>(hr * LIMB) + lo);
+    }
+    ++hc;
+  }
+  __syncthreads();  // the last updates everywhere
+  uint64_t *o = out + (size_t)m * 2 * NN + (size_t)r * NN;
+  for (int c = (int)threadIdx.x; c < NN; c += BR2Y_T) o[c] = to_u64<M>(acs[F::slot_stage(c)]);
+}
+
 }  // namespace omr

@@ -238,9 +238,13 @@ std::vector<CDD> dd_tree_twiddles(int L) {
 // P3 --, level 2 26u -- 5u per premultiplied radix-4 pass --, rounded up), the sequential fma accumulation, and
 // the double-double keys' |K^ - K| <= u |K|. The maximum over every step and output spectrum.
 // kmax: [steps][rows][outputs] (level 1: [512][8][2]; level 2: [670][12][2 out][2 limb], the limbs
-// as two more "outputs").
+// as two more "outputs"). Level 3: level 2 as br2y_kernel (the latency path) accumulates it: each
+// 256-thread group chains its three rows (its j-th at weight 2 (3 - j)), then two additions (the
+// two groups' partials, the partner workgroup's) add 1 each: weight 8 - 2 j for digit 3 g + j.
 double apriori_bound(int level, const std::vector<double> &kmax) {
   const double u = 0x1p-53;
+  const bool y = level == 3;
+  if (y) level = 2;
   const int n = level == 1 ? 512 : 1024, R = level == 1 ? 2 * D1 : 2 * D2, O = level == 1 ? 2 : 4;
   const int steps = level == 1 ? N0 : NI;
   // accumulation order of the kernels' MAC: br1f / br1l rows 0..7; br2f digits in issue order
@@ -257,7 +261,7 @@ double apriori_bound(int level, const std::vector<double> &kmax) {
         const int r = level == 1 ? k : order2[k];
         const double kap = kmax[((size_t)i * R + r) * O + o];
         s += kap;
-        w += (2.0 * R - 2.0 * k) * kap;
+        w += (y ? 8.0 - 2.0 * ((r % D2) % 3) : 2.0 * R - 2.0 * k) * kap;
       }
       worst = std::max(worst, cf * s + cw * w);
     }
@@ -311,6 +315,11 @@ struct omr_ctx {
   bool guard = false, guard_auto[2] = {false, false};
   unsigned long long *margin = nullptr;
   double kappa[2] = {0.0, 0.0}, apriori[2] = {0.0, 0.0}, thr[2] = {1.0, 1.0};
+  // the latency path's level 2 on the FFT (br2y_kernel, opt-in: OMR_BR2Y=1 at context creation)
+  // when its accumulation order's bound (apriori_bound level 3) proves it exact and the level is
+  // not guarded; br2x_kernel's NTT otherwise
+  double apriori_y = 1.0;
+  bool br2y = false;
   // host-API staging
   uint16_t *s_clue_a = nullptr, *s_clue_b = nullptr;
   uint64_t *s_out = nullptr;
@@ -588,7 +597,7 @@ omr_status launch_br2x(omr_ctx *c, size_t n, const uint32_t *lwe_int, uint64_t *
     dev_free(c->x_slots);
     dev_free(c->x_flags);
     c->x_cap = 0;
-    HIP_TRY(hipMalloc(&c->x_slots, n * 4 * N2 * sizeof(double)));
+    HIP_TRY(hipMalloc(&c->x_slots, n * 8 * N2 * sizeof(double)));  // br2y: [n][2][2 slot][2 limb][2][1024]
     HIP_TRY(hipMalloc(&c->x_flags, n * 2 * sizeof(uint32_t)));
     c->x_cap = n;
   }
@@ -600,8 +609,15 @@ omr_status launch_br2x(omr_ctx *c, size_t n, const uint32_t *lwe_int, uint64_t *
   int *err = c->x_err;
   void *args[] = {(void *)&lwe_int, (void *)&bsk2, (void *)&tb, (void *)&slots, (void *)&flags, (void *)&err,
                   (void *)&out};
-  const void *kern = reinterpret_cast<const void *>(&br2x_kernel);
-  const hipError_t e = hipLaunchCooperativeKernel(kern, dim3((unsigned)(2 * n)), dim3(BR2L_T), args, 0, st);
+  // br2y_kernel (FFT) when the bound of its accumulation order proves it exact and level 2 is not
+  // guarded; br2x_kernel's exact NTT otherwise (same arguments apart from the key form)
+  const bool y = c->br2y && !guarded(c, 1) && c->apriori_y < 0.5;
+  const double2 *bskf = c->bsk2f, *twg = c->fft2;
+  void *args_y[] = {(void *)&lwe_int, (void *)&bskf, (void *)&twg, (void *)&tb, (void *)&slots, (void *)&flags,
+                    (void *)&err, (void *)&out};
+  const void *kern = y ? reinterpret_cast<const void *>(&br2y_kernel) : reinterpret_cast<const void *>(&br2x_kernel);
+  const hipError_t e = hipLaunchCooperativeKernel(kern, dim3((unsigned)(2 * n)), dim3(y ? BR2Y_T : BR2L_T),
+                                                  y ? args_y : args, 0, st);
   if (e == hipErrorCooperativeLaunchTooLarge || e == hipErrorNotSupported || e == hipErrorInvalidConfiguration) {
     (void)hipGetLastError();  // refused: nothing was enqueued
     return OMR_OK;
@@ -723,6 +739,8 @@ extern "C" omr_status omr_ctx_create(const omr_detection_key_view *key, int devi
     // processes that made cooperative launches under rocprofv3
     const char *env = getenv("OMR_COOPERATIVE");
     c->coop = coop != 0 && !(env && env[0] == '0');
+    const char *ey = getenv("OMR_BR2Y");
+    c->br2y = ey && ey[0] == '1';
   }
   auto fail = [&](omr_status st) {
     omr_ctx_destroy(c);
@@ -831,6 +849,7 @@ extern "C" omr_status omr_ctx_create(const omr_detection_key_view *key, int devi
     c->kappa[1] = *std::max_element(k2.begin(), k2.end());
     c->apriori[0] = apriori_bound(1, k1);
     c->apriori[1] = apriori_bound(2, k2);
+    c->apriori_y = apriori_bound(3, k2);
     // the exactness contract: a level whose bound does not prove every rounding exact is guarded
     // on every launch and checked against 1 - E (omr_ctx_exactness)
     for (int l = 0; l < 2; ++l) {
