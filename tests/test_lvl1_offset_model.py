@@ -155,16 +155,17 @@ def _digits2_ref(v):
 
 
 def _digits2s(v):
-    y = np.floor(v / 256.0 + 0.5) + 17315143744.0
-    hi = np.floor(y * (1.0 / 2097152.0))
-    lo = y - hi * 2097152.0
-    w0 = u32(lo.astype(np.int64)) ^ 0x102040
-    w1 = u32(hi.astype(np.int64)) ^ 0x2040
+    """Digits2S::pack: the words are the low dword and bits 21..52 of the FP64 pattern of
+    y + 64 (1 + 128 + .. + 128^4) + 1.5 * 2^52 (exact)."""
+    y = np.floor(v / 256.0 + 0.5) + (17315143744.0 + 6755399441055744.0)
+    b = y.view(np.uint64)
+    w0 = u32((b & np.uint64(0xFFFFFFFF)).astype(np.int64)) ^ 0x102040
+    w1 = u32(((b >> np.uint64(21)) & np.uint64(0xFFFFFFFF)).astype(np.int64)) ^ 0x2040
     out = []
     for k in range(6):
         h, j = divmod(k, 3)
         w = s32(w0 if h == 0 else w1)
-        width = 18 if (h == 1 and j == 2) else 7
+        width = 16 if (h == 1 and j == 2) else 7
         f = (w >> (7 * j)) & ((1 << width) - 1)
         out.append(np.where(f >= 1 << (width - 1), f - (1 << width), f))
     return np.stack(out)
@@ -179,3 +180,43 @@ def test_level2_signed_digit_fields_match_digits2():
     assert np.array_equal(_digits2s(v), _digits2_ref(v))
     d = _digits2s(v)
     assert np.array_equal(sum(d[k] * 128 ** k for k in range(6)), np.floor(v / 256.0 + 0.5).astype(np.int64))
+
+
+def test_level2_limb_update_exact():
+    """limb_acc (br2_fft.hpp): acc + lo + 2^25 hr -> the exact centred residue mod q2, in FP64 as the
+    kernel computes it (one quotient, one fma, one red), against Python integers."""
+    Q2 = 1125899906826241
+    q = float(Q2)
+    qinv = 1.0 / q
+    limb = 33554432.0
+    rng = np.random.default_rng(11)
+    n = 200000
+    h2 = Q2 // 2
+    acc = rng.integers(-h2, h2 + 1, n).astype(np.float64)
+    lim = 2 ** 46 - 1
+    lo = rng.integers(-lim, lim + 1, n).astype(np.float64)
+    hr = rng.integers(-lim, lim + 1, n).astype(np.float64)
+    edge = np.array([-h2, h2, 0, 1, -1], dtype=np.float64)
+    acc = np.concatenate([acc, np.repeat(edge, 9)])
+    lo = np.concatenate([lo, np.tile(np.array([-lim, lim, 0], dtype=np.float64), 15)])
+    hr = np.concatenate([hr, np.tile(np.array([lim, -lim, 0], dtype=np.float64).repeat(3), 5)])
+
+    def red(x):
+        return _fma(-np.rint(x * qinv), q, x)
+
+    x = acc + lo
+    hi = hr * limb
+    k = np.rint(_fma(hr, limb * qinv, x * qinv))
+    got = red(_fma(-k, q, hi) + x)
+    for a, l, h, g in zip(acc.astype(np.int64), lo.astype(np.int64), hr.astype(np.int64), got):
+        want = (int(a) + int(l) + (int(h) << 25)) % Q2
+        if want > h2:
+            want -= Q2
+        assert int(g) == want and float(int(g)) == g
+
+
+def _fma(a, b, c):
+    """Correctly rounded a * b + c elementwise (exact rational arithmetic, then one rounding)."""
+    from fractions import Fraction
+    a, b, c = np.broadcast_arrays(np.asarray(a, np.float64), np.asarray(b, np.float64), np.asarray(c, np.float64))
+    return np.array([float(Fraction(x) * Fraction(y) + Fraction(z)) for x, y, z in zip(a.ravel(), b.ravel(), c.ravel())]).reshape(a.shape)

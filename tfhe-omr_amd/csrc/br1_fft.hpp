@@ -52,21 +52,10 @@ struct Lvl1Int {
   // d_3 = y' >> 15 (the same digits as the recursive Digits8<LOGB1, D1, DROP1>). The word kept is
   // y' ^ (16 (1 + 32 + 32^2)): field k then holds d_k in two's complement (d_k + 16 = f in
   // [0, 32) and (f - 16) mod 32 = f ^ 16), the top digit is unchanged, and every digit is one
-  // signed bit-field extract with wave-uniform offset and width (digit()). Returns that word.
+  // signed bit-field extract with wave-uniform offset and width (Lvl1Off::digit_u). Returns that word.
   static constexpr int DIGIT_BIAS = ((1 << (LOGB1 * (D1 - 1))) - 1) / ((1 << LOGB1) - 1) * (1 << (LOGB1 - 1));
   __device__ static __forceinline__ uint32_t digits(int v) {
     return (uint32_t)(((v + (1 << (DROP1 - 1))) >> DROP1) + DIGIT_BIAS) ^ (uint32_t)DIGIT_BIAS;
-  }
-  // signed digit k of a digits() word: one v_bfe_i32 with wave-uniform offset and width
-  // (checked in the listing: v_bfe_i32 + v_cvt_f64_i32; an inline-asm v_bfe_i32 is slower, it
-  // constrains the scheduler).
-  __device__ static __forceinline__ double digit(uint32_t w, int k) {
-    return (double)(int)__builtin_amdgcn_sbfe(w, LOGB1 * k, k < D1 - 1 ? LOGB1 : 32 - LOGB1 * (D1 - 1));
-  }
-  // the same digit by two shifts (the latency kernel measured 1-2 % faster with these)
-  __device__ static __forceinline__ double digit_shifts(uint32_t w, int k) {
-    const int s1 = k < D1 - 1 ? 32 - LOGB1 * (k + 1) : 0, s2 = k < D1 - 1 ? 32 - LOGB1 : LOGB1 * (D1 - 1);
-    return (double)((int)(w << s1) >> s2);
   }
 };
 
@@ -76,7 +65,8 @@ struct Lvl1Int {
 // t = x'' + n = (x - ac) + H (mod Q) with t in (-Q, 2Q), so one v_min3_u32(t, t + Q, t - Q) (the
 // wrapped operands lose) is canon(x - ac) + H in [0, Q), and the digit word of the canonical
 // residue y - H is ((y - H + 2^6 + 2^7 DIGIT_BIAS) >> 7) ^ DIGIT_BIAS (the bias folded in before
-// the shift): 6 integer operations per word (5 in br1l, digits_u). The accumulator update adds a
+// the shift; the shift itself folds into the extraction offsets, digits_u): 5 integer operations
+// per word. The accumulator update adds a
 // rounded product in [0, Q] (Lvl1Int::round_mod): s in [0, 2Q), min(s, s - Q), 3 operations.
 struct Lvl1Off {
   static constexpr uint32_t Q = (uint32_t)Lvl1Int::Q, H = (uint32_t)Lvl1Int::H, OFF = H / 2;
@@ -94,19 +84,20 @@ struct Lvl1Off {
   // the stored negacyclic half "-ac + H/2" and the digit operand
   __device__ static __forceinline__ uint32_t neg(uint32_t acpp) { return H - acpp; }
   // digit word of canon(x - ac) from a stored entry x'' and n = neg(ac''): t = x - ac + H; the
-  // Lvl1Int::digits word (extract with Lvl1Int::digit / digit_shifts)
-  __device__ static __forceinline__ uint32_t digits(uint32_t xs, uint32_t n) {
-    return (uint32_t)((int)digits_u(xs, n) >> DROP1);  // arithmetic: the top digit is signed
-  }
-  // the same word before the shift by DROP1 (bits 7.. hold the fields, bits 0..6 the dropped
-  // remainder, never read): the shift folds into the extraction offsets (digit_shifts_u), one
-  // operation fewer per word. br1l uses it; in br1f the unshifted words changed the register
-  // allocation (9 spills), so br1f keeps the shifted word.
+  // Lvl1Int::digits word before its shift by DROP1 (bits 7.. hold the fields, bits 0..6 the dropped
+  // remainder, never read): the shift folds into the extraction offsets (digit_u / digit_shifts_u),
+  // one operation fewer per word. Both br1l and br1f use it (br1f since round 5: at 248 VGPRs it no
+  // longer spills; same speed, profiles/r05n/bench_variants.log).
   __device__ static __forceinline__ uint32_t digits_u(uint32_t xs, uint32_t n) {
     const uint32_t t = xs + n;
     const uint32_t y = fold(t, t + Q, t - Q);
     constexpr uint32_t C = (uint32_t)((1 << (DROP1 - 1)) - Lvl1Int::H + (Lvl1Int::DIGIT_BIAS << DROP1));
     return (y + C) ^ ((uint32_t)Lvl1Int::DIGIT_BIAS << DROP1);
+  }
+  // signed digit k of a digits_u() word: one v_bfe_i32 at offset DROP1 + 5 k (the top digit: the
+  // word's sign-extended rest)
+  __device__ static __forceinline__ double digit_u(uint32_t w, int k) {
+    return (double)(int)__builtin_amdgcn_sbfe(w, DROP1 + LOGB1 * k, k < D1 - 1 ? LOGB1 : 32 - DROP1 - LOGB1 * (D1 - 1));
   }
   // signed digit k of a digits_u() word by two shifts
   __device__ static __forceinline__ double digit_shifts_u(uint32_t w, int k) {
@@ -152,7 +143,7 @@ __device__ __forceinline__ void br1f_digits(const uint32_t (&ac)[2][16], uint32_
     for (int i = 0; i < 16; ++i) {  // acc_coef(0, i) = 64 i
       uint32_t addr;  // ((b4 + 256 i) & 8191) | sbase in one v_and_or_b32 (not formed by the compiler)
       asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(addr) : "v"(b4 + 256u * i), "s"(kWrap), "v"(sbase));  // one SGPR per VOP3 on gfx9
-      pk[p][i] = Lvl1Off::digits(*(const lds_u32 *)(size_t)addr, n[i]);
+      pk[p][i] = Lvl1Off::digits_u(*(const lds_u32 *)(size_t)addr, n[i]);
     }
     wave_lds_fence();  // the next poly's writes stay below these reads
   }
@@ -219,8 +210,8 @@ __device__ __forceinline__ void br1f_row(const uint32_t (&pk)[16], int k, int q,
   double xr[1][8], xi[1][8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
-    xr[0][e] = Lvl1Int::digit(pk[e], k);
-    xi[0][e] = Lvl1Int::digit(pk[8 + e], k);
+    xr[0][e] = Lvl1Off::digit_u(pk[e], k);
+    xi[0][e] = Lvl1Off::digit_u(pk[8 + e], k);
   }
   F::fwd<1, true>(xr, xi, xch, tws, lane, gtw, w3);
   if (more)

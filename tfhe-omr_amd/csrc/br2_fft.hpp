@@ -257,24 +257,43 @@ __device__ __forceinline__ int key_pos(int t, int e) { return e * Fft1024::T + t
 // d 6, drop 8) with every field a two's-complement digit, so that each digit is one v_bfe_i32
 // (Digits2's biased fields need a v_bfe_u32 and a subtraction of 64). Digits 0..4 are biased by 64
 // as in Digits2 (so the words have no borrows) and each 7-bit field is then XORed with 64
-// ((f - 64) mod 128 = f ^ 64); the top digit d5 is left unbiased, so hi = floor(y / 2^21) holds it
-// as a signed value in bits 14..31 (sign-extended by the extract).
+// ((f - 64) mod 128 = f ^ 64); the top digit d5 is left unbiased, so y >> 21 holds it as a signed
+// value in bits 14..29 (sign-extended by the extract; |y| < 2^42, so |d5| < 2^7).
+// The words come out of the FP64 bit pattern (round 5): Y = y + 1.5 * 2^52 is exact and its low 51
+// mantissa bits are y in two's complement, so lo = Y's low dword (fields 0..2 at bits 0..20; the
+// bits above are never extracted) and hi = bits 21..52 of Y (one v_alignbit_b32): 3 FP64 + 3
+// integer operations per word pair instead of 8 FP64-rate (two floors, two conversions) + 2.
 struct Digits2S {
   static constexpr int DW = 2;
   static_assert(LOGB2 == 7 && D2 == 6 && DROP2 == 8, "closed form written for the level-2 basis");
   __device__ static __forceinline__ void pack(double v, uint32_t (&pk)[DW]) {
-    const double y = floor(__fma_rn(v, 1.0 / 256.0, 0.5)) + 17315143744.0;  // + 64 (1 + 128 + .. + 128^4)
-    const double hi = floor(y * (1.0 / 2097152.0));
-    const double lo = __fma_rn(-hi, 2097152.0, y);
-    pk[0] = (uint32_t)(int)lo ^ 0x102040u;   // fields 0, 1, 2
-    pk[1] = (uint32_t)(int)hi ^ 0x2040u;     // fields 3, 4; d5 in bits 14..
+    // + 64 (1 + 128 + .. + 128^4) + 1.5 * 2^52, an exact double
+    const double y = floor(__fma_rn(v, 1.0 / 256.0, 0.5)) + (17315143744.0 + 6755399441055744.0);
+    const uint64_t b = __builtin_bit_cast(uint64_t, y);
+    const uint32_t lo = (uint32_t)b, hi = (uint32_t)(b >> 32);
+    pk[0] = lo ^ 0x102040u;                                   // fields 0, 1, 2
+    pk[1] = __builtin_amdgcn_alignbit(hi, lo, 21) ^ 0x2040u;  // fields 3, 4; d5 in bits 14..29
   }
+  static constexpr int TOP_WIDTH = 16;  // d5: bits 35..50 of Y
   // digit j + 3 h as a double (h: the word, a compile-time constant)
   template <int H>
   __device__ static __forceinline__ double digit(const uint32_t (&pk)[DW], int j) {
-    return (double)(int)__builtin_amdgcn_sbfe(pk[H], 7 * j, H == 1 && j == 2 ? 18 : 7);
+    return (double)(int)__builtin_amdgcn_sbfe(pk[H], 7 * j, H == 1 && j == 2 ? TOP_WIDTH : 7);
   }
 };
+
+// acc + lo + 2^25 hr, reduced to the exact centred representative mod q2 (acc canonical; lo, hr the
+// rounded limb products, |lo|, |hr| < 2^46): x = acc + lo and 2^25 hr are exact, the quotient
+// k = rint((2^25 hr + x) / q2) is within 2^-30 of the true one, so fma(-k, q2, 2^25 hr) is the exact
+// integer r - x (|r| <= q2 / 2 + 2^21), and one red of r is exact (|r| <= q2 - 1): 12 FP64
+// operations with the two limb roundings instead of 14 (red of the high product, then canon).
+__device__ __forceinline__ double limb_acc(double acc, double lo, double hr) {
+  using M = Mod<2>;
+  const double x = acc + lo;
+  const double hi = hr * LIMB;
+  const double k = rint(__fma_rn(hr, LIMB * M::QINV, x * M::QINV));
+  return canon_small<M>(__fma_rn(-k, M::Q, hi) + x);
+}
 
 // BSK2 (FFT form) through a buffer descriptor: each key load is buffer_load_dwordx4 with the
 // thread's byte offset (t * 16) in voffset and the row / block / register offset in soffset, so a
@@ -362,7 +381,6 @@ template <bool G>
 __device__ __forceinline__ void br2f_update(double *aco, const double (&sr)[2][Fft1024::E],
                                            const double (&si)[2][Fft1024::E], RoundGuard<G> &rg, int t) {
   using F = Fft1024;
-  using M = Mod<2>;
 #pragma unroll
   for (int e = 0; e < F::E; ++e)
 #pragma unroll
@@ -371,9 +389,8 @@ __device__ __forceinline__ void br2f_update(double *aco, const double (&sr)[2][F
       const double lo = rint(ylo), hr = rint(yhi);
       rg.note(ylo, lo);
       rg.note(yhi, hr);
-      const double hi = hr * LIMB;  // exact (|P_hi| < 2^45)
       double &a = aco[F::slot_stage(F::idx(0, t, e) + F::n * h)];
-      a = canon<M>(a + red<M>(hi) + lo);
+      a = limb_acc(a, lo, hr);
     }
 }
 
@@ -617,7 +634,7 @@ __global__ __launch_bounds__(BR2Y_T, 1) void br2y_kernel(const uint32_t *__restr
         for (int e = 0; e < E; ++e) sr[o][l][e] = si[o][l][e] = 0.0;
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
-      const int wd = g == 1 && j == 2 ? 18 : 7;  // the top digit of word 1 is its sign-extended rest
+      const int wd = g == 1 && j == 2 ? Digits2S::TOP_WIDTH : 7;  // the top digit of word 1
       double xr[E], xi[E];
 #pragma unroll
       for (int e = 0; e < E; ++e) {
@@ -738,7 +755,7 @@ __global__ __launch_bounds__(BR2Y_T, 1) void br2y_kernel(const uint32_t *__restr
       const double other = ho[e * T + t];
       const double lo = g == 0 ? lv[0][e] : other, hr = g == 0 ? other : lv[1][e];
       double &acc = acs[F::slot_stage(F::idx(0, t, e) + n * g)];
-      acc = canon<M>(acc + red<M>(hr * LIMB) + lo);
+      acc = limb_acc(acc, lo, hr);
     }
     ++hc;
   }
