@@ -144,9 +144,10 @@ def test_real_keys_stage_parity(real, path):
 
 def test_latency_level2_variants_match_throughput(real):
     """The latency path's level 2 in both forms against the (oracle-checked) throughput kernels,
-    bit for bit: the two-CU kernel br2x at 64 messages (128 workgroups, the default threshold's
-    largest chunk) and the one-CU kernel br2l, which runs when 2 n workgroups exceed the CU count
-    (130 messages with the threshold raised); every output passes the omd KAT."""
+    bit for bit: the two-CU kernel (br2y, the default; br2x is checked against it in
+    test_latency_level2_fft_two_cu_matches_ntt) at 64 messages (128 workgroups, the default
+    threshold's largest chunk) and the one-CU kernel br2l, which runs when 2 n workgroups exceed the
+    CU count (130 messages with the threshold raised); every output passes the omd KAT."""
     a, det, _ = real
     s2 = a.export()["s2"]
     for n, threshold in ((64, 64), (130, 200)):
@@ -167,26 +168,34 @@ def test_latency_level2_variants_match_throughput(real):
 
 
 def test_latency_level2_fft_two_cu_matches_ntt(real, monkeypatch):
-    """The latency path's level 2 on the FFT over two CUs per message (br2y_kernel: a context
-    created with OMR_BR2Y=1; it runs when the a priori bound of its accumulation order is below
-    0.5) against the default exact modular-NTT two-CU kernel (br2x_kernel) on the same level-1
-    outputs, bit for bit, rotation and rotation + trace, at 1, 7 and 64 messages (2, 14 and 128
-    CUs)."""
-    _, ntt, _ = real
+    """The latency path's level 2 on the FFT over two CUs per message (br2y_kernel, the default: it
+    runs when the a priori bound of its accumulation order is below 0.5) against the exact
+    modular-NTT two-CU kernel (br2x_kernel: a context created with OMR_BR2Y=0) on the same level-1
+    outputs, bit for bit, rotation and rotation + trace, at 1, 7, 20 and 64 messages (2, 14, 40 and
+    128 CUs; the first three with four key-prefetch helper workgroups per worker, 64 without), and
+    br2y without its helpers (OMR_PREFETCH=0) at 7."""
+    _, fft, _ = real
     _, _, dk = PL.keys()
-    monkeypatch.setenv("OMR_BR2Y", "1")
-    det = A.Detector(dk)
+    monkeypatch.setenv("OMR_BR2Y", "0")
+    ntt = A.Detector(dk)
     monkeypatch.delenv("OMR_BR2Y")
+    monkeypatch.setenv("OMR_PREFETCH", "0")
+    nopf = A.Detector(dk)
+    monkeypatch.delenv("OMR_PREFETCH")
     try:
-        for n in (1, 7, 64):
+        for n in (1, 7, 20, 64):
             mask = np.zeros(n, dtype=bool)
             mask[::5] = True
             ca, cb = PL.mixed_clues(mask, seed=1200 + n)
-            fl = det.first_level(ca, cb)
-            assert np.array_equal(det.blind_rotate_level2(fl), ntt.blind_rotate_level2(fl)), n
-            assert np.array_equal(det.second_level(fl), ntt.second_level(fl)), n
+            fl = fft.first_level(ca, cb)
+            want = ntt.blind_rotate_level2(fl)
+            assert np.array_equal(fft.blind_rotate_level2(fl), want), n
+            assert np.array_equal(fft.second_level(fl), ntt.second_level(fl)), n
+            if n == 7:
+                assert np.array_equal(nopf.blind_rotate_level2(fl), want)
     finally:
-        det.close()
+        ntt.close()
+        nopf.close()
 
 
 def test_level2_throughput_small_batches(real):

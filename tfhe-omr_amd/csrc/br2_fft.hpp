@@ -559,13 +559,65 @@ __global__ __launch_bounds__(256, 2) void br2f_guard_kernel(const uint32_t *__re
 // otherwise, or on a guarded context, the host runs br2x_kernel's exact NTT instead.
 // LDS: twiddles 16 KB, X0 / X1 of each group 64 KB, the limb swap 32 KB (+ the groups' X1), ACC_r
 // 16 KB: 128 KB, one workgroup per CU.
+// Key prefetchers (round 5): a lone message's workgroup streams 384 KB of FFT-form key per step
+// from HBM / the Infinity Cache at the per-CU rate of a few outstanding loads (~31 GB/s: 8.3 ms of
+// level 2, against 6.1 ms with the key loads skipped, profiles/r05o/); from its XCD's L2 a CU reads
+// ~118 GB/s (tools/microbench_l2.hip). So the launch carries BR2Y_H helper workgroups per worker
+// on the worker's XCD (workgroups b and b + 8 share one: MI355X_MICROARCH.md, §Workgroup dispatch;
+// a placement that differs costs speed, never correctness -- helpers only read the key): helper k
+// touches one dword per 64 B of its quarter of the worker's rows of each executed step, at most
+// BR2Y_PF executed steps ahead of the worker's hand-off count (its flag), so the rows are L2-resident
+// when the worker loads them. Grid: row 0 = the 2n workers (w8 = 2n rounded up to a multiple of 8
+// columns), rows 1..BR2Y_H = the helpers of the worker in the same column; the host launches the
+// helper rows only when every workgroup fits on its own CU.
 constexpr int BR2Y_T = 2 * Fft1024::T;
+constexpr int BR2Y_H = 4, BR2Y_PF = 2;
+
+__device__ __forceinline__ void br2y_prefetch(const uint32_t *__restrict__ lwe_int, const double2 *__restrict__ bskf,
+                                              const uint32_t *flags, int wid, int k) {
+  constexpr int STEP_LINES = D2 * BR2_ROW * (int)sizeof(double2) / 64;  // 64 B lines of one step's rows
+  constexpr int PER_THREAD = STEP_LINES / (BR2Y_H * BR2Y_T);
+  static_assert(PER_THREAD * BR2Y_H * BR2Y_T == STEP_LINES, "helpers split a step's rows evenly");
+  __shared__ int go;
+  const int m = wid >> 1, r = wid & 1;
+  const uint32_t *lwe = lwe_int + (size_t)m * (NI + 1);
+  uint32_t acc = 0;
+  int e = 0;  // executed steps prefetched
+#pragma unroll 1
+  for (int i = 0; i < NI; ++i) {
+    const int a = (int)__builtin_amdgcn_readfirstlane(lwe[i]) & (2 * N2 - 1);
+    if (a == 0) continue;
+    if (threadIdx.x == 0) {  // the worker has published hand-off e - BR2Y_PF (bounded: a helper may give up)
+      int ok = 1, n = 0;
+      while ((int)__hip_atomic_load(flags + wid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < e - BR2Y_PF) {
+        if (++n == (1 << 16)) {
+          ok = 0;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+      go = ok;
+    }
+    __syncthreads();
+    if (!go) break;
+    const char *rows = reinterpret_cast<const char *>(bskf + ((size_t)i * 2 * D2 + (size_t)r * D2) * BR2_ROW);
+    uint32_t v[PER_THREAD];
+#pragma unroll
+    for (int u = 0; u < PER_THREAD; ++u)
+      v[u] = *reinterpret_cast<const uint32_t *>(rows + (size_t)((u * BR2Y_H + k) * BR2Y_T + (int)threadIdx.x) * 64);
+#pragma unroll
+    for (int u = 0; u < PER_THREAD; ++u) acc ^= v[u];
+    __syncthreads();  // thread 0's next poll after every load of this step returned
+    ++e;
+  }
+  asm volatile("" ::"v"(acc));  // the loads stay live
+}
 
 __global__ __launch_bounds__(BR2Y_T, 1) void br2y_kernel(const uint32_t *__restrict__ lwe_int,
                                                          const double2 *__restrict__ bskf,
                                                          const double2 *__restrict__ twg, DeviceTables tb,
                                                          double *xg, uint32_t *flags, int *err,
-                                                         uint64_t *__restrict__ out) {
+                                                         uint64_t *__restrict__ out, int nw, int w8) {
   using F = Fft1024;
   using M = Mod<2>;
   constexpr int E = F::E, NN = N2, n = F::n, T = F::T;
@@ -574,7 +626,13 @@ __global__ __launch_bounds__(BR2Y_T, 1) void br2y_kernel(const uint32_t *__restr
   __shared__ double2 px[2][n];     // [group]: its limb-(1 - g) partial of output 1 - r; the rounded halves
   __shared__ double acs[NN];       // ACC_r
   __shared__ int stop;
-  const int m = blockIdx.x >> 1, r = blockIdx.x & 1;
+  const int wid = (int)blockIdx.x % w8, hrow = (int)blockIdx.x / w8;  // uniform
+  if (wid >= nw) return;
+  if (hrow > 0) {
+    br2y_prefetch(lwe_int, bskf, flags, wid, hrow - 1);
+    return;
+  }
+  const int m = wid >> 1, r = wid & 1;
   const int g = __builtin_amdgcn_readfirstlane((int)threadIdx.x / T), t = (int)threadIdx.x % T;
   const uint32_t *lwe = lwe_int + (size_t)m * (NI + 1);
   if (g == 0) F::load_twiddles(tws, twg, t);

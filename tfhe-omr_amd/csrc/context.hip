@@ -315,11 +315,13 @@ struct omr_ctx {
   bool guard = false, guard_auto[2] = {false, false};
   unsigned long long *margin = nullptr;
   double kappa[2] = {0.0, 0.0}, apriori[2] = {0.0, 0.0}, thr[2] = {1.0, 1.0};
-  // the latency path's level 2 on the FFT (br2y_kernel, opt-in: OMR_BR2Y=1 at context creation)
+  // the latency path's level 2 on the FFT (br2y_kernel with its key-prefetch helpers; the default
+  // since round 5, 6.6 vs 7.6-7.9 ms for br2x at one message; OMR_BR2Y=0 at context creation: br2x)
   // when its accumulation order's bound (apriori_bound level 3) proves it exact and the level is
   // not guarded; br2x_kernel's NTT otherwise
   double apriori_y = 1.0;
-  bool br2y = false;
+  bool br2y = true;
+  bool no_prefetch = false;  // OMR_PREFETCH=0: the latency kernels launch no key-prefetch helpers
   // host-API staging
   uint16_t *s_clue_a = nullptr, *s_clue_b = nullptr;
   uint64_t *s_out = nullptr;
@@ -613,11 +615,15 @@ omr_status launch_br2x(omr_ctx *c, size_t n, const uint32_t *lwe_int, uint64_t *
   // guarded; br2x_kernel's exact NTT otherwise (same arguments apart from the key form)
   const bool y = c->br2y && !guarded(c, 1) && c->apriori_y < 0.5;
   const double2 *bskf = c->bsk2f, *twg = c->fft2;
+  // br2y: the 2n workers in row 0 of a grid w8 = 2n rounded up to 8 columns wide, plus BR2Y_H rows
+  // of key prefetchers (br2_fft.hpp) when every workgroup still gets a CU of its own
+  const int nw = (int)(2 * n), w8 = (nw + 7) / 8 * 8;
+  const int rows = (size_t)w8 * (1 + BR2Y_H) <= (size_t)c->num_cu && !c->no_prefetch ? 1 + BR2Y_H : 1;
   void *args_y[] = {(void *)&lwe_int, (void *)&bskf, (void *)&twg, (void *)&tb, (void *)&slots, (void *)&flags,
-                    (void *)&err, (void *)&out};
+                    (void *)&err, (void *)&out, (void *)&nw, (void *)&w8};
   const void *kern = y ? reinterpret_cast<const void *>(&br2y_kernel) : reinterpret_cast<const void *>(&br2x_kernel);
-  const hipError_t e = hipLaunchCooperativeKernel(kern, dim3((unsigned)(2 * n)), dim3(y ? BR2Y_T : BR2L_T),
-                                                  y ? args_y : args, 0, st);
+  const hipError_t e = hipLaunchCooperativeKernel(kern, dim3(y ? (unsigned)(w8 * rows) : (unsigned)(2 * n)),
+                                                  dim3(y ? BR2Y_T : BR2L_T), y ? args_y : args, 0, st);
   if (e == hipErrorCooperativeLaunchTooLarge || e == hipErrorNotSupported || e == hipErrorInvalidConfiguration) {
     (void)hipGetLastError();  // refused: nothing was enqueued
     return OMR_OK;
@@ -740,7 +746,9 @@ extern "C" omr_status omr_ctx_create(const omr_detection_key_view *key, int devi
     const char *env = getenv("OMR_COOPERATIVE");
     c->coop = coop != 0 && !(env && env[0] == '0');
     const char *ey = getenv("OMR_BR2Y");
-    c->br2y = ey && ey[0] == '1';
+    c->br2y = !(ey && ey[0] == '0');
+    const char *ep = getenv("OMR_PREFETCH");
+    c->no_prefetch = ep && ep[0] == '0';
   }
   auto fail = [&](omr_status st) {
     omr_ctx_destroy(c);

@@ -9,3 +9,4 @@ OMR_GPU_LIB=$A/phase.so tools/gpu_step.sh 300 r05o/phase.log python tools/phase_
 tools/gpu_step.sh 300 r05o/latency_br2x.log python tools/latency_split.py 1 7 || exit 99
 OMR_BR2Y=1 tools/gpu_step.sh 300 r05o/latency_br2y.log python tools/latency_split.py 1 7 || exit 99
 OMR_BR2Y=1 OMR_GPU_LIB=$A/nokey.so tools/gpu_step.sh 300 r05o/latency_br2y_nokey.log python tools/latency_split.py 1 7 || exit 99
+tools/gpu_step.sh 120 r05o/microbench_l2.log tools/microbench_l2 || exit 99
