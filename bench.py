@@ -60,6 +60,14 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
 # FP64 instruction issues in 4 cycles); the arithmetic microbenchmark reaches 95 % of it
 # (profiles/r01_microbench_arith.txt).
 FP64_PEAK_TFLOPS = 256 * 4 * 16 * 2 * 2.4e9 / 1e12
+# L2 -> CU read ceiling: rows every workgroup streams from its XCD's L2, 16 B per lane, 64 KB in
+# flight per workgroup, two workgroups per CU: 30.1-30.6 TB/s chip-wide, 118-120 GB/s per CU
+# (tools/microbench_l2.hip, profiles/r05o/microbench_l2.log).
+L2_CEILING_TBPS = 30.59
+# Key bytes each dominant kernel actually reads from L2 per message, in its device form: br2f the
+# FFT-form BSK2 (670 steps x 12 rows x 2 outputs x 2 limbs x 1024 points x 16 B; no workgroup
+# shares a row), br1f the FFT-form BSK1 rows staged by LDS-DMA once per 4-rotation workgroup.
+L2_KEY_BYTES = {"br2": 670 * 12 * 4 * 1024 * 16, "br1": 7 * 512 * 8 * 2 * 512 * 16 // 4}
 PUBLISHED_CPU_MS_PER_MSG = 234.073003  # README.md:122, 1 thread, AVX-512 CPU (model not stated)
 WEIGHT_SEED = bytes(range(1, 33))
 INDEX_SEED = 9
@@ -231,6 +239,21 @@ def rooflines(role, dom, launches, per_launch_msgs, launch_ms_total, value, worl
                 "valu_issue_frac": round(k.get("valu_lane_instr_per_msg", 0.0) * per_launch_msgs / avg_launch_s
                                          / (FP64_PEAK_TFLOPS / 2 * 1e12), 4),
                 "counts_from": comp.get("source")}
+    if roof is not None and role in L2_KEY_BYTES:
+        l2 = L2_KEY_BYTES[role] * per_launch_msgs / avg_launch_s / 1e12
+        roof["l2_key_stream"] = {"bytes_per_msg": L2_KEY_BYTES[role], "achieved": round(l2, 2),
+                                 "ceiling": L2_CEILING_TBPS, "unit": "TB/s", "frac": round(l2 / L2_CEILING_TBPS, 4),
+                                 "ceiling_from": "tools/microbench_l2.hip (profiles/r05o/microbench_l2.log)"}
+        pk = (pmc or {}).get("kernels", {}).get(dom, {})
+        if pk.get("l2_read_bytes_per_launch") and pmc.get("messages_per_launch"):
+            # every L1 -> L2 read request of the kernel (TCP_TCC_READ_REQ x 128 B), per message: the
+            # key stream plus its twiddle / table / accumulator reads
+            mb = pk["l2_read_bytes_per_launch"] / pmc["messages_per_launch"]
+            roof["l2_key_stream"].update({"measured_bytes_per_msg": round(mb),
+                                          "measured_achieved": round(mb * per_launch_msgs / avg_launch_s / 1e12, 2),
+                                          "l2_hit_rate": None if pk.get("l2_hit_rate") is None
+                                          else round(pk["l2_hit_rate"], 4),
+                                          "measured_from": pmc.get("source")})
     return roof, hbm
 
 
