@@ -173,7 +173,8 @@ def test_latency_level2_fft_two_cu_matches_ntt(real, monkeypatch):
     modular-NTT two-CU kernel (br2x_kernel: a context created with OMR_BR2Y=0) on the same level-1
     outputs, bit for bit, rotation and rotation + trace, at 1, 7, 20 and 64 messages (2, 14, 40 and
     128 CUs; the first three with four key-prefetch helper workgroups per worker, 64 without), and
-    br2y without its helpers (OMR_PREFETCH=0) at 7."""
+    at 7 br2y without its helpers (OMR_PREFETCH=0) and with the sc1 hand-off kept between workers
+    on one XCD (OMR_FAST_HANDOFF=0: the other side of its placement-dependent protocol choice)."""
     _, fft, _ = real
     _, _, dk = PL.keys()
     monkeypatch.setenv("OMR_BR2Y", "0")
@@ -182,6 +183,9 @@ def test_latency_level2_fft_two_cu_matches_ntt(real, monkeypatch):
     monkeypatch.setenv("OMR_PREFETCH", "0")
     nopf = A.Detector(dk)
     monkeypatch.delenv("OMR_PREFETCH")
+    monkeypatch.setenv("OMR_FAST_HANDOFF", "0")
+    slow = A.Detector(dk)
+    monkeypatch.delenv("OMR_FAST_HANDOFF")
     try:
         for n in (1, 7, 20, 64):
             mask = np.zeros(n, dtype=bool)
@@ -193,9 +197,11 @@ def test_latency_level2_fft_two_cu_matches_ntt(real, monkeypatch):
             assert np.array_equal(fft.second_level(fl), ntt.second_level(fl)), n
             if n == 7:
                 assert np.array_equal(nopf.blind_rotate_level2(fl), want)
+                assert np.array_equal(slow.blind_rotate_level2(fl), want)
     finally:
         ntt.close()
         nopf.close()
+        slow.close()
 
 
 def test_level2_throughput_small_batches(real):

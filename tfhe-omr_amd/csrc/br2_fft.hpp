@@ -567,9 +567,19 @@ __global__ __launch_bounds__(256, 2) void br2f_guard_kernel(const uint32_t *__re
 // a placement that differs costs speed, never correctness -- helpers only read the key): helper k
 // touches one dword per 64 B of its quarter of the worker's rows of each executed step, at most
 // BR2Y_PF executed steps ahead of the worker's hand-off count (its flag), so the rows are L2-resident
-// when the worker loads them. Grid: row 0 = the 2n workers (w8 = 2n rounded up to a multiple of 8
-// columns), rows 1..BR2Y_H = the helpers of the worker in the same column; the host launches the
-// helper rows only when every workgroup fits on its own CU.
+// when the worker loads them.
+// Same-XCD hand-off (round 5): the hand-off cost 1.2 of br2y's 6.6 ms (profiles/r05t: its payload
+// stores, poll and loads removed in a timing-only build) -- an sc1 store writes the line through and
+// drops it from L2, so the partner's loads go beyond L2. Both workers of a message are therefore
+// placed in one grid column (so on one XCD when the dispatcher deals blocks round-robin), each reads
+// its XCD id (HW_REG_XCC_ID) and they swap it through global memory with sc1 accesses once per
+// launch. When the ids agree, the payload and the flag are written with plain stores, which stay in
+// that XCD's L2 where the partner's sc1 loads (L1 bypassed) find them; otherwise the sc1 protocol
+// above runs unchanged. Either way every payload load is an sc1 load, so the choice follows the
+// actual placement and changes speed only.
+// Grid: w8 = n rounded up to a multiple of 8 columns (message m in column m); row 0 = the mask
+// workers, row 1 = the body workers, rows 2 + 2k + r = helper k of worker (m, r); the host launches
+// the helper rows only when every workgroup fits on its own CU. flags[2n .. 4n): the XCD ids + 1.
 constexpr int BR2Y_T = 2 * Fft1024::T;
 constexpr int BR2Y_H = 4, BR2Y_PF = 2;
 
@@ -617,7 +627,8 @@ __global__ __launch_bounds__(BR2Y_T, 1) void br2y_kernel(const uint32_t *__restr
                                                          const double2 *__restrict__ bskf,
                                                          const double2 *__restrict__ twg, DeviceTables tb,
                                                          double *xg, uint32_t *flags, int *err,
-                                                         uint64_t *__restrict__ out, int nw, int w8) {
+                                                         uint64_t *__restrict__ out, int nmsg, int w8,
+                                                         int allow_fast) {
   using F = Fft1024;
   using M = Mod<2>;
   constexpr int E = F::E, NN = N2, n = F::n, T = F::T;
@@ -625,15 +636,18 @@ __global__ __launch_bounds__(BR2Y_T, 1) void br2y_kernel(const uint32_t *__restr
   __shared__ double2 xb[2][2][n];  // [group][X0, X1]
   __shared__ double2 px[2][n];     // [group]: its limb-(1 - g) partial of output 1 - r; the rounded halves
   __shared__ double acs[NN];       // ACC_r
-  __shared__ int stop;
-  const int wid = (int)blockIdx.x % w8, hrow = (int)blockIdx.x / w8;  // uniform
-  if (wid >= nw) return;
-  if (hrow > 0) {
-    br2y_prefetch(lwe_int, bskf, flags, wid, hrow - 1);
+  __shared__ int stop, same_xcd;
+  const int m = (int)blockIdx.x % w8, row = (int)blockIdx.x / w8;  // uniform
+  if (m >= nmsg) return;
+  if (row >= 2) {
+    br2y_prefetch(lwe_int, bskf, flags, 2 * m + ((row - 2) & 1), (row - 2) >> 1);
     return;
   }
-  const int m = wid >> 1, r = wid & 1;
+  const int r = row, wid = 2 * m + r;
   const int g = __builtin_amdgcn_readfirstlane((int)threadIdx.x / T), t = (int)threadIdx.x % T;
+  const int pslot = __builtin_amdgcn_readfirstlane(wid < 2 ? 8 + 8 * wid + (int)(threadIdx.x >> 6) : -1);
+  (void)pslot;
+  OMR_PHASE_CLOCK(pslot, 0);
   const uint32_t *lwe = lwe_int + (size_t)m * (NI + 1);
   if (g == 0) F::load_twiddles(tws, twg, t);
   {  // ACC_r = X^{-b} * LUT2 (body) or 0 (mask)
@@ -641,13 +655,28 @@ __global__ __launch_bounds__(BR2Y_T, 1) void br2y_kernel(const uint32_t *__restr
     const int rr = (2 * NN - (b % (2 * NN))) % (2 * NN);
     for (int c = (int)threadIdx.x; c < NN; c += BR2Y_T)
       acs[F::slot_stage(c)] = r == 1 ? canon_small<M>(rot_read<NN>(tb.lut2, c, rr)) : 0.0;
-    if (threadIdx.x == 0) stop = 0;
+    if (threadIdx.x == 0) {
+      stop = 0;
+      // XCD ids through global memory (sc1 both ways); a partner that never answers leaves the
+      // sc1 protocol in place (the step loop's bounded poll then reports it)
+      uint32_t *xid = flags + 2 * nmsg;
+      const uint32_t mine = (uint32_t)__builtin_amdgcn_s_getreg(6164) + 1u;  // hwreg(HW_REG_XCC_ID, 0, 4)
+      __hip_atomic_store(xid + wid, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      uint32_t theirs = 0;
+      for (int k = 0; k < (1 << 20) && theirs == 0; ++k) {
+        theirs = __hip_atomic_load(xid + (wid ^ 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (theirs == 0) __builtin_amdgcn_s_sleep(2);
+      }
+      same_xcd = allow_fast && theirs == mine;
+    }
   }
   double2 wc[4][2];  // this thread's forward twiddles of passes 1..4
   F::block_ct<1>(wc[0], twg, t);
   F::block_ct<2>(wc[1], twg, t);
   F::block_ct<3>(wc[2], twg, t);
   F::block_ct<4>(wc[3], twg, t);
+  __syncthreads();  // same_xcd (and the accumulator) visible
+  const bool fast = __builtin_amdgcn_readfirstlane(same_xcd) != 0;
   const __amdgpu_buffer_rsrc_t rsrc = bsk2_rsrc(bskf);
   const uint32_t t16 = (uint32_t)t * 16u;
   uint32_t *my_flag = flags + 2 * m + r, *their_flag = flags + 2 * m + (1 - r);
@@ -658,6 +687,7 @@ __global__ __launch_bounds__(BR2Y_T, 1) void br2y_kernel(const uint32_t *__restr
   for (int i = 0; i < NI; ++i) {
     const int a = (int)__builtin_amdgcn_readfirstlane(lwe[i]) & (2 * NN - 1);
     if (a == 0) continue;  // (X^0 - 1) * ACC = 0 (both workgroups of the message skip it)
+    OMR_PHASE(pslot, (int)hc, 0);
     const int q0 = i * 2 * D2 + r * D2 + 3 * g;  // the group's first GGSW row of this step
 #ifdef OMR_BR2Y_NOKEY
 #define br2y_load(...) ((void)0)
@@ -683,6 +713,7 @@ __global__ __launch_bounds__(BR2Y_T, 1) void br2y_kernel(const uint32_t *__restr
 #pragma unroll
         for (int e = 0; e < E; ++e) pw[h][e] = g ? pk[h][e][1] : pk[h][e][0];
     }
+    OMR_PHASE(pslot, (int)hc, 1);
     double sr[2][2][E], si[2][2][E];  // [output][limb] partial spectra of the group's three digits
 #pragma unroll
     for (int o = 0; o < 2; ++o)
@@ -718,6 +749,7 @@ __global__ __launch_bounds__(BR2Y_T, 1) void br2y_kernel(const uint32_t *__restr
         }
       }
     }
+    OMR_PHASE(pslot, (int)hc, 2);
     // the four partials by role (r and g are uniform: selects, no dynamic register indexing):
     // [0] output r limb g (kept), [1] output r limb 1 - g, [2] output 1 - r limb g (handed to the
     // partner), [3] output 1 - r limb 1 - g
@@ -748,6 +780,7 @@ __global__ __launch_bounds__(BR2Y_T, 1) void br2y_kernel(const uint32_t *__restr
       }
     }
     wg_barrier_lds();
+    OMR_PHASE(pslot, (int)hc, 3);
     double fr[E], fi[E];  // limb g of output r: this workgroup's six rows, then the partner's six
     {
       const double2 *qr = xb[1 - g][1], *qh = px[1 - g];
@@ -758,14 +791,32 @@ __global__ __launch_bounds__(BR2Y_T, 1) void br2y_kernel(const uint32_t *__restr
         const double2 vr = qr[e * T + t], vh = qh[e * T + t];
         fr[e] = pr4[0][e] + vr.x;
         fi[e] = pi4[0][e] + vr.y;
-        st_sc1(dst + e * T + t, pr4[2][e] + vh.x);  // limb g of output 1 - r: the partner's
-        st_sc1(dst + n + e * T + t, pi4[2][e] + vh.y);
+#ifndef OMR_BR2Y_NOHANDOFF  // timing-only ablation: no payload crosses (wrong output)
+        if (fast) {  // plain stores: the lines stay in this XCD's L2 for the partner's sc1 loads
+          dst[e * T + t] = pr4[2][e] + vh.x;
+          dst[n + e * T + t] = pi4[2][e] + vh.y;
+        } else {
+          st_sc1(dst + e * T + t, pr4[2][e] + vh.x);  // limb g of output 1 - r: the partner's
+          st_sc1(dst + n + e * T + t, pi4[2][e] + vh.y);
+        }
+#else
+        (void)dst;
+        (void)vh;
+        (void)their_flag;
+#endif
       }
+#ifndef OMR_BR2Y_NOHANDOFF
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
     }
     __syncthreads();
+    OMR_PHASE(pslot, (int)hc, 4);
     if (threadIdx.x == 0) {
-      __hip_atomic_store(my_flag, hc + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (fast)
+        __hip_atomic_store(my_flag, hc + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);  // plain store
+      else
+        __hip_atomic_store(my_flag, hc + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#ifndef OMR_BR2Y_NOHANDOFF
       int k = 0;
       while (__hip_atomic_load(their_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < hc + 1) {
         if (++k == BR2X_SPIN) {
@@ -775,15 +826,21 @@ __global__ __launch_bounds__(BR2Y_T, 1) void br2y_kernel(const uint32_t *__restr
         }
         __builtin_amdgcn_s_sleep(2);
       }
+#endif
     }
     __syncthreads();
+    OMR_PHASE(pslot, (int)hc, 5);
     if (stop) break;
     {  // the partner's limb g of output r
       const double *src = xg + ((((size_t)m * 2 + (1 - r)) * 2 + (hc & 1)) * 2 + g) * 2 * n;
 #pragma unroll
       for (int e = 0; e < E; ++e) {
+#ifndef OMR_BR2Y_NOHANDOFF
         fr[e] += ld_sc1(src + e * T + t);
         fi[e] += ld_sc1(src + n + e * T + t);
+#else
+        (void)src;
+#endif
       }
     }
     asm volatile("" : "+v"(fr[0]), "+v"(fr[1]), "+v"(fr[2]), "+v"(fr[3]), "+v"(fi[0]), "+v"(fi[1]), "+v"(fi[2]),
@@ -796,6 +853,7 @@ __global__ __launch_bounds__(BR2Y_T, 1) void br2y_kernel(const uint32_t *__restr
     }
 #endif
     F::inv(fr, fi, xb[g][1], tws, t);  // X1: every reader of the limb swap passed the hand-off barriers
+    OMR_PHASE(pslot, (int)hc, 6);
     // round limb g; the groups swap halves: group g recombines the coefficients idx(0, t, e) + 1024 g
     double lv[2][E];  // [h][e]: limb g of coefficient idx(0, t, e) + 1024 h
 #pragma unroll
@@ -815,8 +873,10 @@ __global__ __launch_bounds__(BR2Y_T, 1) void br2y_kernel(const uint32_t *__restr
       double &acc = acs[F::slot_stage(F::idx(0, t, e) + n * g)];
       acc = limb_acc(acc, lo, hr);
     }
+    OMR_PHASE(pslot, (int)hc, 7);
     ++hc;
   }
+  OMR_PHASE_CLOCK(pslot, 1);
   __syncthreads();  // the last updates everywhere
   uint64_t *o = out + (size_t)m * 2 * NN + (size_t)r * NN;
   for (int c = (int)threadIdx.x; c < NN; c += BR2Y_T) o[c] = to_u64<M>(acs[F::slot_stage(c)]);

@@ -322,6 +322,7 @@ struct omr_ctx {
   double apriori_y = 1.0;
   bool br2y = true;
   bool no_prefetch = false;  // OMR_PREFETCH=0: the latency kernels launch no key-prefetch helpers
+  bool no_fast_handoff = false;  // OMR_FAST_HANDOFF=0: br2y keeps the sc1 hand-off on one XCD too
   // host-API staging
   uint16_t *s_clue_a = nullptr, *s_clue_b = nullptr;
   uint64_t *s_out = nullptr;
@@ -600,10 +601,10 @@ omr_status launch_br2x(omr_ctx *c, size_t n, const uint32_t *lwe_int, uint64_t *
     dev_free(c->x_flags);
     c->x_cap = 0;
     HIP_TRY(hipMalloc(&c->x_slots, n * 8 * N2 * sizeof(double)));  // br2y: [n][2][2 slot][2 limb][2][1024]
-    HIP_TRY(hipMalloc(&c->x_flags, n * 2 * sizeof(uint32_t)));
+    HIP_TRY(hipMalloc(&c->x_flags, n * 4 * sizeof(uint32_t)));  // br2y: + the workers' XCD ids
     c->x_cap = n;
   }
-  HIP_TRY(hipMemsetAsync(c->x_flags, 0, n * 2 * sizeof(uint32_t), st));
+  HIP_TRY(hipMemsetAsync(c->x_flags, 0, n * 4 * sizeof(uint32_t), st));
   const double *bsk2 = c->bsk2;
   DeviceTables tb = c->tb;
   double *slots = c->x_slots;
@@ -615,12 +616,14 @@ omr_status launch_br2x(omr_ctx *c, size_t n, const uint32_t *lwe_int, uint64_t *
   // guarded; br2x_kernel's exact NTT otherwise (same arguments apart from the key form)
   const bool y = c->br2y && !guarded(c, 1) && c->apriori_y < 0.5;
   const double2 *bskf = c->bsk2f, *twg = c->fft2;
-  // br2y: the 2n workers in row 0 of a grid w8 = 2n rounded up to 8 columns wide, plus BR2Y_H rows
-  // of key prefetchers (br2_fft.hpp) when every workgroup still gets a CU of its own
-  const int nw = (int)(2 * n), w8 = (nw + 7) / 8 * 8;
-  const int rows = (size_t)w8 * (1 + BR2Y_H) <= (size_t)c->num_cu && !c->no_prefetch ? 1 + BR2Y_H : 1;
+  // br2y: message m in column m of a grid w8 = n rounded up to 8 columns wide, its mask / body
+  // workers in rows 0 / 1, plus 2 BR2Y_H rows of key prefetchers (br2_fft.hpp) when every workgroup
+  // still gets a CU of its own
+  const int nmsg = (int)n, w8 = (nmsg + 7) / 8 * 8, allow_fast = c->no_fast_handoff ? 0 : 1;
+  const int rows = (size_t)w8 * (2 + 2 * BR2Y_H) <= (size_t)c->num_cu && !c->no_prefetch ? 2 + 2 * BR2Y_H : 2;
+  if (y && (size_t)w8 * rows > (size_t)c->num_cu) return OMR_OK;  // one workgroup per CU: br2l instead
   void *args_y[] = {(void *)&lwe_int, (void *)&bskf, (void *)&twg, (void *)&tb, (void *)&slots, (void *)&flags,
-                    (void *)&err, (void *)&out, (void *)&nw, (void *)&w8};
+                    (void *)&err, (void *)&out, (void *)&nmsg, (void *)&w8, (void *)&allow_fast};
   const void *kern = y ? reinterpret_cast<const void *>(&br2y_kernel) : reinterpret_cast<const void *>(&br2x_kernel);
   const hipError_t e = hipLaunchCooperativeKernel(kern, dim3(y ? (unsigned)(w8 * rows) : (unsigned)(2 * n)),
                                                   dim3(y ? BR2Y_T : BR2L_T), y ? args_y : args, 0, st);
@@ -749,6 +752,8 @@ extern "C" omr_status omr_ctx_create(const omr_detection_key_view *key, int devi
     c->br2y = !(ey && ey[0] == '0');
     const char *ep = getenv("OMR_PREFETCH");
     c->no_prefetch = ep && ep[0] == '0';
+    const char *eh = getenv("OMR_FAST_HANDOFF");
+    c->no_fast_handoff = eh && eh[0] == '0';
   }
   auto fail = [&](omr_status st) {
     omr_ctx_destroy(c);

@@ -3,6 +3,7 @@
 Runs one single-message detect (latency path) and prints the mean cycles between consecutive phase
 marks of executed steps 200..263 for every traced wave (br1l workgroup 0; br2x workgroups 0, 1)."""
 import ctypes
+import os
 import sys
 
 sys.path.insert(0, "tests")
@@ -31,9 +32,12 @@ names = {  # phase ending at mark k (k = 1..7); br2x has no mark 2 (a mark there
              5: "outs read", 6: "inverse", 7: "update + barrier3"},
     "br2x": {1: "stage+digits", 3: "3 fwd + MAC + g1 partial + barrier", 4: "g0 sum + sc1 stores + vmcnt + barrier",
              5: "flag + poll + barrier", 6: "sc1 loads + inverse (g0) / barrier (g1)", 7: "update"},
+    "br2y": {1: "barrier + digits", 2: "3 fwd + MAC", 3: "limb-swap writes + barrier",
+             4: "sums + sc1 stores + vmcnt + barrier", 5: "flag + poll + barrier", 6: "sc1 loads + inverse",
+             7: "round + half swap + barrier + update"},
 }
 for slot in range(24):
-    kern = "br1l" if slot < 8 else "br2x"
+    kern = "br1l" if slot < 8 else ("br2x" if os.environ.get("OMR_BR2Y") == "0" else "br2y")
     m = marks[slot]
     if not m[:, 0].any():
         continue
