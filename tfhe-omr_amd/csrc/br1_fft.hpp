@@ -270,25 +270,33 @@ __device__ __forceinline__ void br1f_step_lds(uint32_t (&ac)[2][16], double2 *xc
 // g. The transforms are wave-private (wave-level LDS sync); the waves run the CMUX steps in
 // lockstep, sharing each key row staged in LDS and one twiddle table.
 // G: the rounding-margin guard (exactness.hpp) publishes the largest |y - rint(y)| to *margin.
+// LDS of br1f_body, carved from a pool (so that dual_kernel can overlay it with br2f_body's):
+// the exchange buffers (8 KB-aligned: br1f_digits' addressing), the twiddles, the LWE masks, the two
+// staged key rows: 76 KB.
+constexpr size_t BR1_LDS_XCH = 0, BR1_LDS_TWS = BR1_LDS_XCH + (size_t)BR1F_WPG * Fft512::BUF * sizeof(double2),
+                 BR1_LDS_LA = BR1_LDS_TWS + (size_t)Fft512::N * sizeof(double2),
+                 BR1_LDS_KBUF = BR1_LDS_LA + (size_t)BR1F_WPG * N0 * sizeof(uint16_t),
+                 BR1_LDS_BYTES = BR1_LDS_KBUF + 2 * (size_t)KROW_SLOTS * sizeof(double2);
+
 template <bool G>
 __device__ __forceinline__ void br1f_body(
     const uint16_t *__restrict__ clue_a, const uint16_t *__restrict__ clue_b,
     const uint16_t *__restrict__ lwe_a, const uint16_t *__restrict__ lwe_b,
     const double2 *__restrict__ bskf, DeviceTables tb, uint32_t *__restrict__ ext,
-    uint64_t *__restrict__ rlwe_out, int mode, size_t nrot, unsigned long long *margin) {
+    uint64_t *__restrict__ rlwe_out, int mode, size_t nrot, unsigned long long *margin, char *pool, size_t item) {
   constexpr int NF = Fft512::N, W = BR1F_WPG;
   static_assert(16 % W == 0, "LDS key staging: W divides the row's 16 one-KiB pieces");
-  __shared__ __attribute__((aligned(8192))) double2 xch_all[W][Fft512::BUF];  // br1f_digits' addressing
   static_assert(Fft512::BUF * sizeof(double2) == 8192, "one 8 KB buffer per wave");
-  __shared__ double2 tws[NF];
-  __shared__ uint16_t la_all[W][N0];
-  __shared__ double2 kbuf[2 * KROW_SLOTS];
+  double2(&xch_all)[W][Fft512::BUF] = *reinterpret_cast<double2(*)[W][Fft512::BUF]>(pool + BR1_LDS_XCH);
+  double2 *tws = reinterpret_cast<double2 *>(pool + BR1_LDS_TWS);
+  uint16_t(&la_all)[W][N0] = *reinterpret_cast<uint16_t(*)[W][N0]>(pool + BR1_LDS_LA);
+  double2 *kbuf = reinterpret_cast<double2 *>(pool + BR1_LDS_KBUF);
   // the wave index is wave-uniform: readfirstlane keeps it (and every key-row DMA address and M0
   // value derived from it) in SGPRs instead of per-lane VALU arithmetic
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   double2 *xch = xch_all[wave];
   uint16_t *la = la_all[wave];
-  const size_t g = (size_t)blockIdx.x * W + wave;
+  const size_t g = item * W + wave;
   const size_t gi = g < nrot ? g : nrot - 1;  // a tail slot recomputes the last rotation
   int b;
   if (lwe_a == nullptr) {  // extract clue c of message m (CmLweCiphertext::extract_all, :514)
@@ -357,14 +365,16 @@ __global__ __launch_bounds__(64 * BR1F_WPG, 2) void br1f_kernel(
     const uint16_t *__restrict__ lwe_a, const uint16_t *__restrict__ lwe_b,
     const double2 *__restrict__ bskf, DeviceTables tb, uint32_t *__restrict__ ext,
     uint64_t *__restrict__ rlwe_out, int mode, size_t nrot) {
-  br1f_body<false>(clue_a, clue_b, lwe_a, lwe_b, bskf, tb, ext, rlwe_out, mode, nrot, nullptr);
+  __shared__ __attribute__((aligned(8192))) char pool[BR1_LDS_BYTES];
+  br1f_body<false>(clue_a, clue_b, lwe_a, lwe_b, bskf, tb, ext, rlwe_out, mode, nrot, nullptr, pool, blockIdx.x);
 }
 __global__ __launch_bounds__(64 * BR1F_WPG, 2) void br1f_guard_kernel(
     const uint16_t *__restrict__ clue_a, const uint16_t *__restrict__ clue_b,
     const uint16_t *__restrict__ lwe_a, const uint16_t *__restrict__ lwe_b,
     const double2 *__restrict__ bskf, DeviceTables tb, uint32_t *__restrict__ ext,
     uint64_t *__restrict__ rlwe_out, int mode, size_t nrot, unsigned long long *margin) {
-  br1f_body<true>(clue_a, clue_b, lwe_a, lwe_b, bskf, tb, ext, rlwe_out, mode, nrot, margin);
+  __shared__ __attribute__((aligned(8192))) char pool[BR1_LDS_BYTES];
+  br1f_body<true>(clue_a, clue_b, lwe_a, lwe_b, bskf, tb, ext, rlwe_out, mode, nrot, margin, pool, blockIdx.x);
 }
 
 // Test entry (omr_fft1_mul): out = a * k mod (X^1024 + 1, q1) through the level-1 FFT path,

@@ -409,21 +409,26 @@ __device__ __forceinline__ void br2f_update(double *aco, const double (&sr)[2][F
 // use rewrites a buffer whose readers have passed a later barrier: 17 workgroup barriers per step
 // (one at the step start: the previous update visible to the rotated reads).
 // LDS: twiddles 16 KB, X0 / X1 32 KB, ACC 32 KB (80 KB: two workgroups per CU).
+// LDS of br2f_body, carved from a pool (dual_kernel overlays it with br1f_body's): the twiddles,
+// then X0, X1, ACC (mask, body); the trace's 3 N2 doubles afterwards: 80 KB.
+constexpr size_t BR2_LDS_X = 0, BR2_LDS_TWS = 4 * (size_t)Fft1024::n * sizeof(double2),
+                 BR2_LDS_BYTES = BR2_LDS_TWS + (size_t)Fft1024::n * sizeof(double2);
+
 template <bool G>
 __device__ __forceinline__ void br2f_body(const uint32_t *__restrict__ lwe_int, const double2 *__restrict__ bskf,
                                           const double2 *__restrict__ twg, const double *__restrict__ tk,
                                           DeviceTables tb, uint64_t *__restrict__ out, int mode,
-                                          unsigned long long *margin) {
+                                          unsigned long long *margin, double2 *pool, size_t item) {
   using F = Fft1024;
   using M = Mod<2>;
   constexpr int E = F::E, NN = N2;
   static_assert(F::TW_LEN <= F::n, "the twiddle table's LDS doubles as the trace's NTT table");
-  __shared__ double2 tws[F::n];
-  __shared__ double2 lds[4][F::n];  // X0, X1, ACC (mask, body); the trace's 3 N2 doubles afterwards
+  double2 *tws = pool + BR2_LDS_TWS / sizeof(double2);
+  double2(&lds)[4][F::n] = *reinterpret_cast<double2(*)[4][F::n]>(pool + BR2_LDS_X / sizeof(double2));
   double2(&Xb)[2][F::n] = *reinterpret_cast<double2(*)[2][F::n]>(&lds[0][0]);
   double *acs = reinterpret_cast<double *>(&lds[2][0]);
   const int t = threadIdx.x;
-  const uint32_t *lwe = lwe_int + (size_t)blockIdx.x * (NI + 1);
+  const uint32_t *lwe = lwe_int + item * (NI + 1);
   F::load_twiddles(tws, twg, t);
   {  // ACC = (0, X^{-b} * LUT2)
     const int b = (int)lwe[NI];
@@ -490,7 +495,7 @@ __device__ __forceinline__ void br2f_body(const uint32_t *__restrict__ lwe_int, 
   }
   rg.publish(margin);
   __syncthreads();  // the last updates everywhere
-  uint64_t *o = out + (size_t)blockIdx.x * 2 * NN;
+  uint64_t *o = out + item * 2 * NN;
   if (mode == 1) {
 #pragma unroll
     for (int p = 0; p < 2; ++p)
@@ -526,14 +531,16 @@ __global__ __launch_bounds__(256, 2) void br2f_kernel(const uint32_t *__restrict
                                                       const double2 *__restrict__ bskf,
                                                       const double2 *__restrict__ twg, const double *__restrict__ tk,
                                                       DeviceTables tb, uint64_t *__restrict__ out, int mode) {
-  br2f_body<false>(lwe_int, bskf, twg, tk, tb, out, mode, nullptr);
+  __shared__ double2 pool[BR2_LDS_BYTES / sizeof(double2)];
+  br2f_body<false>(lwe_int, bskf, twg, tk, tb, out, mode, nullptr, pool, blockIdx.x);
 }
 __global__ __launch_bounds__(256, 2) void br2f_guard_kernel(const uint32_t *__restrict__ lwe_int,
                                                             const double2 *__restrict__ bskf,
                                                             const double2 *__restrict__ twg, const double *__restrict__ tk,
                                                             DeviceTables tb, uint64_t *__restrict__ out, int mode,
                                                             unsigned long long *margin) {
-  br2f_body<true>(lwe_int, bskf, twg, tk, tb, out, mode, margin);
+  __shared__ double2 pool[BR2_LDS_BYTES / sizeof(double2)];
+  br2f_body<true>(lwe_int, bskf, twg, tk, tb, out, mode, margin, pool, blockIdx.x);
 }
 
 

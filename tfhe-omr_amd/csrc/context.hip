@@ -18,6 +18,7 @@
 
 #include "br2_fft.hpp"
 #include "detect_kernels.hpp"
+#include "dual_kernel.hpp"
 #include "encode_kernels.hpp"
 #include "key_spectra.hpp"
 #include "latency_kernels.hpp"
@@ -323,6 +324,11 @@ struct omr_ctx {
   bool br2y = true;
   bool no_prefetch = false;  // OMR_PREFETCH=0: the latency kernels launch no key-prefetch helpers
   bool no_fast_handoff = false;  // OMR_FAST_HANDOFF=0: br2y keeps the sc1 hand-off on one XCD too
+  // co-scheduled levels (dual_kernel.hpp): OMR_DUAL=1 at context creation; a detect call of D
+  // messages is cut into dual_chunks chunks so that level 1 of chunk k + 1 runs beside level 2 of k
+  bool dual = false;
+  int dual_chunks = 8;
+  unsigned *dual_ctl = nullptr;
   // host-API staging
   uint16_t *s_clue_a = nullptr, *s_clue_b = nullptr;
   uint64_t *s_out = nullptr;
@@ -754,6 +760,10 @@ extern "C" omr_status omr_ctx_create(const omr_detection_key_view *key, int devi
     c->no_prefetch = ep && ep[0] == '0';
     const char *eh = getenv("OMR_FAST_HANDOFF");
     c->no_fast_handoff = eh && eh[0] == '0';
+    const char *ed = getenv("OMR_DUAL");
+    c->dual = ed && ed[0] == '1';
+    const char *ec = getenv("OMR_DUAL_CHUNKS");
+    if (ec && atoi(ec) >= 2) c->dual_chunks = atoi(ec);
   }
   auto fail = [&](omr_status st) {
     omr_ctx_destroy(c);
@@ -914,6 +924,7 @@ extern "C" void omr_ctx_destroy(omr_ctx *c) {
   dev_free(c->ks_part);
   dev_free(c->x_slots);
   dev_free(c->x_flags);
+  dev_free(c->dual_ctl);
   dev_free(c->t_slots);
   dev_free(c->t_flags);
   dev_free(c->margin);
@@ -1037,6 +1048,20 @@ namespace {
 
 constexpr int EV_PER_CHUNK = 5;
 
+// Level 1 of B1 messages (clues ca1 / cb1 -> c->ext) beside level 2 + trace of B2 messages
+// (c->lwe_int -> out2) in one dual_kernel launch.
+omr_status launch_dual(omr_ctx *c, size_t B1, const uint16_t *ca1, const uint16_t *cb1, size_t B2, uint64_t *out2,
+                       hipStream_t st) {
+  if (!c->dual_ctl) HIP_TRY(hipMalloc(&c->dual_ctl, DUAL_CTL_WORDS * sizeof(unsigned)));
+  HIP_TRY(hipMemsetAsync(c->dual_ctl, 0, DUAL_CTL_WORDS * sizeof(unsigned), st));
+  const size_t nrot = B1 * CLUES;
+  const unsigned n1 = (unsigned)((nrot + BR1F_WPG - 1) / BR1F_WPG), n2 = (unsigned)B2;
+  dual_kernel<<<n1 + n2, 256, 0, st>>>(ca1, cb1, c->bsk1f, c->ext, nrot, n1, c->lwe_int, c->bsk2f, c->fft2, c->tk,
+                                       out2, n2, c->tb, c->dual_ctl);
+  HIP_TRY(hipGetLastError());
+  return OMR_OK;
+}
+
 // Detect D messages of device buffers on st, in chunks of c->batch: per chunk br1f (7 rotations
 // per message) -> sum7 -> key switch -> br2 + trace. Stage events per chunk: [0] br1 start,
 // [1] br1 end, [2] key switch end, [3] level-2 rotation end, [4] trace end ([3] = [4] when the
@@ -1059,6 +1084,52 @@ omr_status detect_device(omr_ctx *c, const uint16_t *ca, const uint16_t *cb, siz
     c->timed_split = true;
   }
   if ((s = scratch_acquire(c, st)) != OMR_OK) return s;
+  // co-scheduled levels (dual_kernel.hpp): chunks of about D / dual_chunks; level 1 of the first,
+  // then per chunk k + 1 one dual launch (its level 1 beside chunk k's level 2), sum7 and key
+  // switch, and chunk k's level 2 (the last alone). Stage events: [0] / [1] around chunk k's level 1
+  // (the dual launch that carries it), [2] after its key switch, [3] = [4] after the launch that
+  // carries its level 2 -- the two levels overlap, so the split is of launches, not of levels.
+  const size_t per = (D + c->dual_chunks - 1) / c->dual_chunks;
+  if (c->dual && !split && !guarded(c, 0) && !guarded(c, 1) && D >= 2 && !latency_path(c, std::min(per, c->batch))) {
+    const size_t B = std::min(per, c->batch), nch = (D + B - 1) / B;
+    if (c->timing) {
+      while (c->events.size() < nch * EV_PER_CHUNK) {
+        hipEvent_t e;
+        HIP_TRY(hipEventCreate(&e));
+        c->events.push_back(e);
+      }
+      c->timed_chunks = nch;
+      c->timed_split = false;
+    }
+    auto ev = [&](size_t ch, int k) -> omr_status {
+      if (c->timing) HIP_TRY(hipEventRecord(c->events[ch * EV_PER_CHUNK + k], st));
+      return OMR_OK;
+    };
+    auto front = [&](size_t ch) -> omr_status {  // chunk ch: sum7 + key switch after its level 1
+      const int Bc = (int)std::min(B, D - ch * B);
+      const size_t n7 = (size_t)Bc * (N1 + 1);
+      sum7_kernel<<<(unsigned)((n7 + 255) / 256), 256, 0, st>>>(c->ext, c->lwe1t, Bc);
+      omr_status r;
+      if ((r = launch_ks(c, Bc, c->lwe_int, st)) != OMR_OK) return r;
+      return ev(ch, 2);
+    };
+    if ((s = ev(0, 0)) != OMR_OK) return s;
+    if ((s = launch_br1(c, std::min(B, D) * CLUES, ca, cb, nullptr, nullptr, c->ext, nullptr, 0, st,
+                        std::min(B, D))) != OMR_OK)
+      return s;
+    if ((s = ev(0, 1)) != OMR_OK || (s = front(0)) != OMR_OK) return s;
+    for (size_t ch = 0; ch + 1 < nch; ++ch) {
+      const size_t o1 = (ch + 1) * B, B1 = std::min(B, D - o1), o2 = ch * B;
+      if ((s = ev(ch + 1, 0)) != OMR_OK) return s;
+      if ((s = launch_dual(c, B1, ca + o1 * N0, cb + o1 * CLUES, B, out + o2 * 2 * N2, st)) != OMR_OK) return s;
+      if ((s = ev(ch + 1, 1)) != OMR_OK || (s = ev(ch, 3)) != OMR_OK || (s = ev(ch, 4)) != OMR_OK) return s;
+      if ((s = front(ch + 1)) != OMR_OK) return s;
+    }
+    const size_t ol = (nch - 1) * B;
+    if ((s = launch_br2(c, D - ol, c->lwe_int, out + ol * 2 * N2, 0, st, false, nullptr)) != OMR_OK) return s;
+    if ((s = ev(nch - 1, 3)) != OMR_OK || (s = ev(nch - 1, 4)) != OMR_OK) return s;
+    return scratch_release(c, st);
+  }
   for (size_t ch = 0; ch < nchunks; ++ch) {
     const size_t off = ch * c->batch;
     const int B = (int)std::min(c->batch, D - off);
