@@ -56,3 +56,13 @@ def apriori_bound_latency2(dk, q2=1125899906826241):
     hi = np.rint(r2 / 2.0 ** 25)
     k2 = np.stack([_row_max(r2 - hi * 2.0 ** 25, 1024), _row_max(hi, 1024)], axis=-1).reshape(670, 12, 4)
     return _bound(k2, 1024, 12, 64.0, list(range(12)), 41 + 26, [8 - 2 * ((r % 6) % 3) for r in range(12)])
+
+
+def apriori_bound_trace(dk, q2=1125899906826241):
+    """The FFT trace (br2f_trace; context.hip, apriori_bound level 4): 11 steps, 25 rows of the trace
+    key [11][25][2 out][2048] as two 25-bit limbs, digits |d| <= 3 (balanced base 4, the top one in
+    [-2, 3]), accumulated in row order."""
+    r = _centred(dk.trace_key.reshape(11, 25, 2, 2048), q2)
+    hi = np.rint(r / 2.0 ** 25)
+    k = np.stack([_row_max(r - hi * 2.0 ** 25, 1024), _row_max(hi, 1024)], axis=-1).reshape(11, 25, 4)
+    return _bound(k, 1024, 25, 3.0, list(range(25)), 41 + 26)

@@ -44,3 +44,14 @@ def test_header_declares_the_contract():
     hdr = open(os.path.join(ROOT, "include", "omr_gpu.h")).read()
     assert "OMR_ERR_INEXACT = 5" in hdr
     assert "omr_status omr_ctx_exactness(omr_ctx *ctx, int guarded[2], uint64_t breaches[2]);" in hdr
+
+
+def test_trace_fft_bound_far_below_level2():
+    """The FFT trace's a priori bound (digits |d| <= 3 over 25 rows) on a uniform key: far below 0.5
+    and below level 2's, so trace_fft_kernel runs on every real key (context.hip: trace_fft)."""
+    dk = _uniform_key()
+    rng = np.random.default_rng(9)
+    dk.trace_key = rng.integers(0, CK.Q2, size=(11, 25, 2, 2048), dtype=np.uint64)
+    et = FB.apriori_bound_trace(dk)
+    _, e2, _, _ = FB.apriori_bounds(dk)
+    assert 0 < et < 0.5 and et < e2, (et, e2)

@@ -254,7 +254,8 @@ def test_two_contexts_concurrent_latency_chunks():
 def test_detect_time_info_split():
     """Timing mode 2 (the reference's DetectTimeInfo split) runs the throughput path's level-2
     rotation and trace as two launches: identical output, the trace timed on its own, and the
-    stages sum to the total; mode 1 (the production fused kernel) reports the trace inside level 2."""
+    stages sum to the total; mode 1 likewise (since round 5 the production path runs the FFT trace
+    as its own launch, trace_fft_kernel)."""
     a, b, dk = PL.keys()
     det = A.Detector(dk)
     det.set_latency_threshold(0)
@@ -271,7 +272,7 @@ def test_detect_time_info_split():
     assert t2["trace_separate"] == 1 and t2["trace_ms"] > 0 and t2["messages"] == 200
     assert t2["first_level_ms"] > t2["key_switch_ms"] > 0 and t2["second_level_ms"] > 0
     assert abs(t2["total_ms"] - t2["first_level_ms"] - t2["second_level_ms"] - t2["trace_ms"]) < 1e-3 * t2["total_ms"] + 1e-3
-    assert t1["trace_separate"] == 0 and t1["trace_ms"] < 0.05 * t1["second_level_ms"]
+    assert t1["trace_separate"] == 1 and 0 < t1["trace_ms"] < 0.2 * t1["second_level_ms"]
     assert abs(t1["total_ms"] - t1["first_level_ms"] - t1["second_level_ms"] - t1["trace_ms"]) < 1e-3 * t1["total_ms"] + 1e-3
 
 

@@ -220,3 +220,41 @@ def _fma(a, b, c):
     from fractions import Fraction
     a, b, c = np.broadcast_arrays(np.asarray(a, np.float64), np.asarray(b, np.float64), np.asarray(c, np.float64))
     return np.array([float(Fraction(x) * Fraction(y) + Fraction(z)) for x, y, z in zip(a.ravel(), b.ravel(), c.ravel())]).reshape(a.shape)
+
+
+def _trace_digits_recursive(v):
+    """DigitsTrace's reference: d = y - 4 floor(y / 4 + 1/2), 24 times, then the rest (the oracle's
+    recursive NonPowOf2ApproxSignedBasis form for base 4, 25 digits)."""
+    y = v.copy()
+    out = []
+    for _ in range(24):
+        c = np.floor(y * 0.25 + 0.5)
+        out.append((y - 4 * c).astype(np.int64))
+        y = c
+    out.append(y.astype(np.int64))
+    return np.stack(out)
+
+
+def _trace_digits_closed(v):
+    """DigitsTrace::pack / get_int (detect_kernels.hpp): the dwords of v + 2 (1 + .. + 4^23) + 1.5 2^52
+    with every 2-bit field XORed with 2, two's-complement 2-bit fields, the top one 3 bits at 48."""
+    b = (v + (187649984473770.0 + 6755399441055744.0)).view(np.uint64)
+    w0 = s32(u32((b & np.uint64(0xFFFFFFFF)).astype(np.int64)) ^ 0xAAAAAAAA)
+    w1 = s32(u32((b >> np.uint64(32)).astype(np.int64)) ^ 0xAAAA)
+    out = []
+    for k in range(25):
+        w, off, width = (w0, 2 * k, 2) if k < 16 else (w1, 2 * (k - 16), 3 if k == 24 else 2)
+        f = (w >> off) & ((1 << width) - 1)
+        out.append(np.where(f >= 1 << (width - 1), f - (1 << width), f))
+    return np.stack(out)
+
+
+def test_trace_digit_closed_form_matches_recursive():
+    Q2 = 1125899906826241
+    h2 = Q2 // 2
+    rng = np.random.default_rng(5)
+    v = np.concatenate([rng.integers(-h2, h2 + 1, 300000), np.array([-h2, h2, 0, 1, -1, 2, -2, 3, -3]),
+                        np.arange(-3000, 3000) * 4 ** 12 + 2 * (4 ** 12 - 1) // 3]).astype(np.float64)
+    d = _trace_digits_closed(v)
+    assert np.array_equal(d, _trace_digits_recursive(v))
+    assert np.array_equal(sum(d[k] * 4 ** k for k in range(25)), v.astype(np.int64))

@@ -394,6 +394,125 @@ __device__ __forceinline__ void br2f_update(double *aco, const double (&sr)[2][F
     }
 }
 
+// hom_trace (detector.rs:626-639; secret.rs:167-168 for N^-1) on the exact FFT (round 5), in place on
+// the LDS-resident accumulator (acs: mask, body at slot_stage positions, canonical): c *= N^-1, then
+// for each of the 11 automorphisms sigma_g: c += KS_g(sigma_g(c)), where the key switch decomposes
+// sigma_g(a) into 25 balanced base-4 digits (DigitsTrace) and multiply-accumulates them with the
+// trace key's rows exactly as a CMUX step does with BSK2's: the same Fft1024 transforms, the key as
+// two 25-bit limbs (tkf: [11 * 25 rows][2 out][2 limb][1024], x 1/1024, row q = 11 k + d ... in
+// the order k * 25 + d), the four inverses rounded to the exact limb products and recombined mod q2
+// (limb_acc). Both halves stay in the coefficient domain, where sigma_g is the signed permutation
+// trace_src; A goes to the mask, sigma_g(b) + B to the body. Each digit's products are below
+// 2 * 2^24 * 2048 * 25 < 2^42 (|d| <= 2 for 24 of them, 3 for the top one), so the a priori bound
+// of this accumulation (apriori_bound level 4) is far below level 2's; the host falls back to the
+// NTT trace when it is not below 0.5. 25 transforms of 120 FP64 operations per thread and step
+// instead of 25 modular NTTs of ~450.
+template <bool G>
+__device__ __forceinline__ void br2f_trace(double *acs, const double2 *__restrict__ tkf, double2 (&Xb)[2][Fft1024::n],
+                                           const double2 *tws, const double2 *__restrict__ twg, const DeviceTables &tb,
+                                           RoundGuard<G> &rg, int t) {
+  using F = Fft1024;
+  using M = Mod<2>;
+  constexpr int E = F::E, NN = N2;
+  double2 wc[4][2];  // the forward twiddles again (not kept live across the rotation)
+  F::block_ct<1>(wc[0], twg, t);
+  F::block_ct<2>(wc[1], twg, t);
+  F::block_ct<3>(wc[2], twg, t);
+  F::block_ct<4>(wc[3], twg, t);
+  constexpr double NINV = -549755813880.0;  // 2048^-1 mod q2 = 1125350151012361, centred
+  static_assert(DT == 25 && TRACE_STEPS == 11, "trace geometry");
+#pragma unroll
+  for (int p = 0; p < 2; ++p)
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        double &x = acs[p * NN + F::slot_stage(F::idx(0, t, e) + F::n * h)];
+        x = canon<M>(mm<M>(x, NINV));
+      }
+  constexpr uint32_t bytes = (uint32_t)((size_t)TRACE_STEPS * DT * BR2_ROW * sizeof(double2));
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<double2 *>(tkf), 0, bytes, 0x00020000);
+  const uint32_t t16 = (uint32_t)t * 16u;
+#pragma unroll 1
+  for (int k = 0; k < TRACE_STEPS; ++k) {
+    const uint16_t *src = tb.trace_src + k * NN;
+    double2 ka[2][E], kb[2][E];
+    br2f_load_half(ka, rsrc, k * DT, 0, t16);
+    __syncthreads();  // the previous update (or the scaling) visible
+    uint32_t pk[2][E][DigitsTrace::DW];  // sigma_g(a) at the thread's P0 points (coefficients j, j + 1024)
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const int sidx = src[F::idx(0, t, e) + F::n * h];
+        const double v = sidx < NN ? acs[F::slot_stage(sidx)] : -acs[F::slot_stage(sidx - NN)];
+        DigitsTrace::pack(v, pk[h][e]);
+        asm volatile("" : "+v"(pk[h][e][0]), "+v"(pk[h][e][1]));
+      }
+    double sr[2][2][E], si[2][2][E];  // [output A / B][limb]
+#pragma unroll
+    for (int o = 0; o < 2; ++o)
+#pragma unroll
+      for (int l = 0; l < 2; ++l)
+#pragma unroll
+        for (int e = 0; e < E; ++e) sr[o][l][e] = si[o][l][e] = 0.0;
+#pragma unroll 1
+    for (int d = 0; d < DT; ++d) {
+      const int q = k * DT + d;
+      double xr[E], xi[E];
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        xr[e] = DigitsTrace::get(pk[0][e], d);
+        xi[e] = DigitsTrace::get(pk[1][e], d);
+      }
+      F::fwd(xr, xi, Xb[d & 1], t, wc);
+      br2f_load_half(kb, rsrc, q, 1, t16);
+#pragma unroll
+      for (int o = 0; o < 2; ++o) {
+#pragma unroll
+        for (int l = 0; l < 2; ++l)
+#pragma unroll
+          for (int e = 0; e < E; ++e) {
+            const double2 kv = o ? kb[l][e] : ka[l][e];
+            sr[o][l][e] = __fma_rn(xr[e], kv.x, __fma_rn(-xi[e], kv.y, sr[o][l][e]));
+            si[o][l][e] = __fma_rn(xr[e], kv.y, __fma_rn(xi[e], kv.x, si[o][l][e]));
+          }
+        if (o == 0) br2f_load_half(ka, rsrc, d + 1 < DT ? q + 1 : q, 0, t16);
+      }
+    }
+    // the four inverses on X0, X1, X0, X1 (the digits' last use of X1 was two uses back)
+#pragma unroll
+    for (int o = 0; o < 2; ++o)
+#pragma unroll
+      for (int l = 0; l < 2; ++l) F::inv(sr[o][l], si[o][l], Xb[l], tws, t);
+    double sb[2][E];  // sigma_g(b) at the thread's coefficients, read before any thread updates acs
+    const uint16_t *srcb = src;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const int sidx = srcb[F::idx(0, t, e) + F::n * h];
+        sb[h][e] = sidx < NN ? acs[NN + F::slot_stage(sidx)] : -acs[NN + F::slot_stage(sidx - NN)];
+      }
+    __syncthreads();  // every thread has read sigma_g(a) and sigma_g(b)
+#pragma unroll
+    for (int e = 0; e < E; ++e)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int c = F::slot_stage(F::idx(0, t, e) + F::n * h);
+        const double alo = h ? si[0][0][e] : sr[0][0][e], ahi = h ? si[0][1][e] : sr[0][1][e];
+        const double blo = h ? si[1][0][e] : sr[1][0][e], bhi = h ? si[1][1][e] : sr[1][1][e];
+        const double ral = rint(alo), rah = rint(ahi), rbl = rint(blo), rbh = rint(bhi);
+        rg.note(alo, ral);
+        rg.note(ahi, rah);
+        rg.note(blo, rbl);
+        rg.note(bhi, rbh);
+        acs[c] = limb_acc(acs[c], ral, rah);
+        acs[NN + c] = limb_acc(acs[NN + c] + sb[h][e], rbl, rbh);
+      }
+  }
+}
+
 // Level-2 blind rotation (BlindRotationKey::blind_rotate, detector.rs:623) on the exact FFT: one
 // 256-thread workgroup per message; output the coefficient-domain rotation (mode 1) or, after
 // hom_trace (detector.rs:626-639), the NttRlweCiphertext (mode 0).
@@ -416,8 +535,7 @@ constexpr size_t BR2_LDS_X = 0, BR2_LDS_TWS = 4 * (size_t)Fft1024::n * sizeof(do
 
 template <bool G>
 __device__ __forceinline__ void br2f_body(const uint32_t *__restrict__ lwe_int, const double2 *__restrict__ bskf,
-                                          const double2 *__restrict__ twg, const double *__restrict__ tk,
-                                          DeviceTables tb, uint64_t *__restrict__ out, int mode,
+                                          const double2 *__restrict__ twg, DeviceTables tb, uint64_t *__restrict__ out,
                                           unsigned long long *margin, double2 *pool, size_t item) {
   using F = Fft1024;
   using M = Mod<2>;
@@ -496,51 +614,97 @@ __device__ __forceinline__ void br2f_body(const uint32_t *__restrict__ lwe_int, 
   rg.publish(margin);
   __syncthreads();  // the last updates everywhere
   uint64_t *o = out + item * 2 * NN;
-  if (mode == 1) {
 #pragma unroll
-    for (int p = 0; p < 2; ++p)
+  for (int p = 0; p < 2; ++p)
 #pragma unroll
-      for (int h = 0; h < 2; ++h)
+    for (int h = 0; h < 2; ++h)
 #pragma unroll
-        for (int e = 0; e < E; ++e) {
-          const int c = F::idx(0, t, e) + F::n * h;
-          o[p * NN + c] = to_u64<M>(acs[p * NN + F::slot_stage(c)]);
-        }
-    return;
-  }
-  // hom_trace on the accumulator in the trace NTTs' coefficient layout (t + 256 e, 8 per thread)
-  double acc0[BR2_E], acc1[BR2_E];
+      for (int e = 0; e < E; ++e) {
+        const int c = F::idx(0, t, e) + F::n * h;
+        o[p * NN + c] = to_u64<M>(acs[p * NN + F::slot_stage(c)]);
+      }
+}
+
+// The trace as its own launch on the FFT (trace_fft_kernel, round 5): in place on level 2's
+// coefficient-domain output (canonical u64 [2][N2] per message) -> NttRlweCiphertext. br2f_body's
+// LDS layout (X0, X1, ACC, twiddles: 80 KB, two workgroups per CU); br2f_trace, then both halves
+// to the NTT domain. Its own launch, not fused into br2f_kernel: fused, the trace's live values
+// pushed the rotation loop to 37-53 VGPR spills.
+template <bool G>
+__device__ __forceinline__ void trace_fft_body(uint64_t *__restrict__ io, const double2 *__restrict__ tkf,
+                                               const double2 *__restrict__ twg, DeviceTables tb,
+                                               unsigned long long *margin) {
+  using F = Fft1024;
+  using M = Mod<2>;
+  constexpr int E = F::E, NN = N2;
+  __shared__ double2 pool[BR2_LDS_BYTES / sizeof(double2)];
+  double2 *tws = pool + BR2_LDS_TWS / sizeof(double2);
+  double2(&lds)[4][F::n] = *reinterpret_cast<double2(*)[4][F::n]>(pool + BR2_LDS_X / sizeof(double2));
+  double2(&Xb)[2][F::n] = *reinterpret_cast<double2(*)[2][F::n]>(&lds[0][0]);
+  double *acs = reinterpret_cast<double *>(&lds[2][0]);
+  const int t = threadIdx.x;
+  uint64_t *o = io + (size_t)blockIdx.x * 2 * NN;
+  F::load_twiddles(tws, twg, t);
+#pragma unroll
+  for (int p = 0; p < 2; ++p)
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const int c = F::idx(0, t, e) + F::n * h;
+        acs[p * NN + F::slot_stage(c)] = from_u64<M>(o[p * NN + c]);
+      }
+  RoundGuard<G> rg;
+  br2f_trace<G>(acs, tkf, Xb, tws, twg, tb, rg, t);
+  rg.publish(margin);
+  __syncthreads();  // the last updates everywhere
+  // to_ntt_rlwe: both halves to the NTT domain (the trace NTTs' coefficient layout t + 256 e)
+  using NTT = WgNtt<M, BR2_T, BR2_E>;
+  double ca[BR2_E], cb[BR2_E];
 #pragma unroll
   for (int e = 0; e < BR2_E; ++e) {
-    acc0[e] = acs[F::slot_stage(t + e * BR2_T)];
-    acc1[e] = acs[NN + F::slot_stage(t + e * BR2_T)];
+    ca[e] = acs[F::slot_stage(t + e * BR2_T)];
+    cb[e] = acs[NN + F::slot_stage(t + e * BR2_T)];
   }
-  double *xch = reinterpret_cast<double *>(&lds[0][0]);  // 3 N2 doubles
+  double *xch = reinterpret_cast<double *>(&lds[0][0]);  // 2 N2 doubles (below the accumulator)
   double *tw = reinterpret_cast<double *>(tws);           // N2 doubles
+  static_assert(NTT::LDS_DOUBLES * sizeof(double) <= 2 * F::n * sizeof(double2), "NTT exchange below ACC");
+#pragma unroll
+  for (int e = 0; e < BR2_E; ++e) tw[t + e * BR2_T] = tb.tw2[t + e * BR2_T];
   __syncthreads();
+  NTT::fwd(ca, xch, tw, t);
+  NTT::fwd(cb, xch, tw, t);
 #pragma unroll
   for (int e = 0; e < BR2_E; ++e) {
-    tw[t + e * BR2_T] = tb.tw2[t + e * BR2_T];
-    xch[2 * NN + t + e * BR2_T] = tb.itw2[t + e * BR2_T];
+    const int j = t * BR2_E + e;
+    o[j] = to_u64<M>(canon<M>(ca[e]));
+    o[NN + j] = to_u64<M>(canon<M>(cb[e]));
   }
-  __syncthreads();
-  hom_trace_store(acc0, acc1, xch, tw, xch + 2 * NN, tk, tb, o, t);
+}
+__global__ __launch_bounds__(256, 2) void trace_fft_kernel(uint64_t *__restrict__ io, const double2 *__restrict__ tkf,
+                                                           const double2 *__restrict__ twg, DeviceTables tb) {
+  trace_fft_body<false>(io, tkf, twg, tb, nullptr);
+}
+__global__ __launch_bounds__(256, 2) void trace_fft_guard_kernel(uint64_t *__restrict__ io,
+                                                                 const double2 *__restrict__ tkf,
+                                                                 const double2 *__restrict__ twg, DeviceTables tb,
+                                                                 unsigned long long *margin) {
+  trace_fft_body<true>(io, tkf, twg, tb, margin);
 }
 
 __global__ __launch_bounds__(256, 2) void br2f_kernel(const uint32_t *__restrict__ lwe_int,
                                                       const double2 *__restrict__ bskf,
-                                                      const double2 *__restrict__ twg, const double *__restrict__ tk,
-                                                      DeviceTables tb, uint64_t *__restrict__ out, int mode) {
+                                                      const double2 *__restrict__ twg, DeviceTables tb,
+                                                      uint64_t *__restrict__ out) {
   __shared__ double2 pool[BR2_LDS_BYTES / sizeof(double2)];
-  br2f_body<false>(lwe_int, bskf, twg, tk, tb, out, mode, nullptr, pool, blockIdx.x);
+  br2f_body<false>(lwe_int, bskf, twg, tb, out, nullptr, pool, blockIdx.x);
 }
 __global__ __launch_bounds__(256, 2) void br2f_guard_kernel(const uint32_t *__restrict__ lwe_int,
                                                             const double2 *__restrict__ bskf,
-                                                            const double2 *__restrict__ twg, const double *__restrict__ tk,
-                                                            DeviceTables tb, uint64_t *__restrict__ out, int mode,
-                                                            unsigned long long *margin) {
+                                                            const double2 *__restrict__ twg, DeviceTables tb,
+                                                            uint64_t *__restrict__ out, unsigned long long *margin) {
   __shared__ double2 pool[BR2_LDS_BYTES / sizeof(double2)];
-  br2f_body<true>(lwe_int, bskf, twg, tk, tb, out, mode, margin, pool, blockIdx.x);
+  br2f_body<true>(lwe_int, bskf, twg, tb, out, margin, pool, blockIdx.x);
 }
 
 

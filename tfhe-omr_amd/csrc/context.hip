@@ -242,16 +242,19 @@ std::vector<CDD> dd_tree_twiddles(int L) {
 // as two more "outputs"). Level 3: level 2 as br2y_kernel (the latency path) accumulates it: each
 // 256-thread group chains its three rows (its j-th at weight 2 (3 - j)), then two additions (the
 // two groups' partials, the partner workgroup's) add 1 each: weight 8 - 2 j for digit 3 g + j.
+// Level 4: the fused FFT trace (br2f_trace): 11 steps, 25 rows (digits |d| <= 3) accumulated in
+// order, the trace key's rows [11 * 25][2 out][2 limb] as kmax.
 double apriori_bound(int level, const std::vector<double> &kmax) {
   const double u = 0x1p-53;
-  const bool y = level == 3;
-  if (y) level = 2;
-  const int n = level == 1 ? 512 : 1024, R = level == 1 ? 2 * D1 : 2 * D2, O = level == 1 ? 2 : 4;
-  const int steps = level == 1 ? N0 : NI;
+  const bool y = level == 3, tr = level == 4;
+  if (y || tr) level = 2;
+  const int n = level == 1 ? 512 : 1024, R = level == 1 ? 2 * D1 : tr ? DT : 2 * D2, O = level == 1 ? 2 : 4;
+  const int steps = level == 1 ? N0 : tr ? TRACE_STEPS : NI;
   // accumulation order of the kernels' MAC: br1f / br1l rows 0..7; br2f digits in issue order
   // g = 2 j + w, row p D2 + j + 3 w (br2_fft.hpp)
   const int order2[12] = {0, 3, 1, 4, 2, 5, 6, 9, 7, 10, 8, 11};
-  const double D = std::sqrt(2.0 * n) * (level == 1 ? 16.0 : 64.0);
+  // largest digit: level 1 16, level 2 64, the trace's balanced base-4 digits 2 (the top one 3)
+  const double D = std::sqrt(2.0 * n) * (level == 1 ? 16.0 : tr ? 3.0 : 64.0);
   const double dft = level == 1 ? 37 + 32 : 41 + 26;  // delta_fwd + delta_inv, in units of u
   const double cf = dft * u + u * (1 + 0x1p-40), cw = std::sqrt(2.0) * u;
   double worst = 0.0;
@@ -259,7 +262,7 @@ double apriori_bound(int level, const std::vector<double> &kmax) {
     for (int o = 0; o < O; ++o) {
       double s = 0.0, w = 0.0;
       for (int k = 0; k < R; ++k) {
-        const int r = level == 1 ? k : order2[k];
+        const int r = level == 1 || tr ? k : order2[k];
         const double kap = kmax[((size_t)i * R + r) * O + o];
         s += kap;
         w += (y ? 8.0 - 2.0 * ((r % D2) % 3) : 2.0 * R - 2.0 * k) * kap;
@@ -283,6 +286,7 @@ struct omr_ctx {
   double2 *fft1 = nullptr;   // level-1 FFT twiddles
   double *bsk2 = nullptr, *tk = nullptr;  // BSK2 NTT domain (latency kernels), trace key
   double2 *bsk2f = nullptr;                // BSK2 as FFT-domain 25-bit limbs (br2f_kernel), x 1/1024
+  double2 *tkf = nullptr;                  // the trace key the same way (br2f_kernel's fused trace)
   double2 *fft2 = nullptr;                 // Fft1024 twiddles
   uint32_t *kskb = nullptr;  // int8 limbs of the KSK, [1024][4][672][32] (matrix-core key switch)
   double *tables = nullptr;  // tw1 itw1 tw2 itw2 lut1 lut2 tw2c
@@ -316,6 +320,10 @@ struct omr_ctx {
   bool guard = false, guard_auto[2] = {false, false};
   unsigned long long *margin = nullptr;
   double kappa[2] = {0.0, 0.0}, apriori[2] = {0.0, 0.0}, thr[2] = {1.0, 1.0};
+  // the fused trace on the FFT (br2f_trace) when its a priori bound (apriori_bound level 4) is below
+  // 0.5; otherwise br2f_kernel stops at the rotation and trace_kernel's NTT runs (never on a real key)
+  double apriori_t = 1.0;
+  bool trace_fft = false;
   // the latency path's level 2 on the FFT (br2y_kernel with its key-prefetch helpers; the default
   // since round 5, 6.6 vs 7.6-7.9 ms for br2x at one message; OMR_BR2Y=0 at context creation: br2x)
   // when its accumulation order's bound (apriori_bound level 3) proves it exact and the level is
@@ -689,24 +697,38 @@ omr_status launch_br2(omr_ctx *c, size_t n, const uint32_t *lwe_int, uint64_t *o
     if (!two_cu) br2l_kernel<<<(unsigned)n, BR2L_T, 0, st>>>(lwe_int, c->bsk2, c->tb, out);
     split_trace = true;
   } else {
-    const int m = split_trace && mode == 0 ? 1 : mode;
-    if (guarded(c, 1)) {
-      // the exactness contract: a launch whose margin reaches 1 - E2 is re-run on the exact NTT
-      // (br2l_fallback_kernel: every workgroup leaves at once otherwise), its trace too when fused
-      omr_status s;
-      if ((s = guard_begin(c, 1, st)) != OMR_OK) return s;
-      br2f_guard_kernel<<<(unsigned)n, Fft1024::T, 0, st>>>(lwe_int, c->bsk2f, c->fft2, c->tk, c->tb, out, m,
-                                                            c->margin + 3);
+    // br2f_kernel (the rotation, coefficient domain), then the trace as its own launch: on the FFT
+    // (trace_fft_kernel) when its a priori bound allows, else the NTT (trace_kernel). The exactness
+    // contract: a guarded pair notes both kernels' rounding margins in level 2's word, and a launch
+    // pair whose margin reaches the threshold is re-run on the exact NTT (br2l_fallback_kernel and
+    // trace_fallback_kernel: every workgroup leaves at once otherwise).
+    const bool g = guarded(c, 1);
+    omr_status s;
+    if (g && (s = guard_begin(c, 1, st)) != OMR_OK) return s;
+    if (g)
+      br2f_guard_kernel<<<(unsigned)n, Fft1024::T, 0, st>>>(lwe_int, c->bsk2f, c->fft2, c->tb, out, c->margin + 3);
+    else
+      br2f_kernel<<<(unsigned)n, Fft1024::T, 0, st>>>(lwe_int, c->bsk2f, c->fft2, c->tb, out);
+    HIP_TRY(hipGetLastError());
+    if (mid) HIP_TRY(hipEventRecord(mid, st));
+    if (mode == 0) {
+      if (!c->trace_fft)
+        trace_kernel<<<(unsigned)n, BR2_T, 0, st>>>(out, c->tk, c->tb);
+      else if (g)
+        trace_fft_guard_kernel<<<(unsigned)n, Fft1024::T, 0, st>>>(out, c->tkf, c->fft2, c->tb, c->margin + 3);
+      else
+        trace_fft_kernel<<<(unsigned)n, Fft1024::T, 0, st>>>(out, c->tkf, c->fft2, c->tb);
       HIP_TRY(hipGetLastError());
+    }
+    if (g) {
       br2l_fallback_kernel<<<(unsigned)n, BR2L_T, 0, st>>>(lwe_int, c->bsk2, c->tb, out, c->margin + 3, c->thr[1]);
       HIP_TRY(hipGetLastError());
-      if (m == 0)
+      if (mode == 0)
         trace_fallback_kernel<<<(unsigned)n, BR2_T, 0, st>>>(out, c->tk, c->tb, c->margin + 3, c->thr[1]);
       HIP_TRY(hipGetLastError());
       if ((s = guard_end(c, 1, st)) != OMR_OK) return s;
-    } else {
-      br2f_kernel<<<(unsigned)n, Fft1024::T, 0, st>>>(lwe_int, c->bsk2f, c->fft2, c->tk, c->tb, out, m);
     }
+    return OMR_OK;
   }
   HIP_TRY(hipGetLastError());
   if (mid) HIP_TRY(hipEventRecord(mid, st));
@@ -841,6 +863,7 @@ extern "C" omr_status omr_ctx_create(const omr_detection_key_view *key, int devi
       hipMalloc(&c->bsk2, BSK2_ELEMS * sizeof(double)) != hipSuccess ||
       hipMalloc(&c->bsk2f, BSK2_ELEMS * sizeof(double2)) != hipSuccess ||
       hipMalloc(&c->tk, TK_ELEMS * sizeof(double)) != hipSuccess ||
+      hipMalloc(&c->tkf, TK_ELEMS * sizeof(double2)) != hipSuccess ||
       hipMalloc(&c->kskb, KSKB_WORDS * sizeof(uint32_t)) != hipSuccess)
     return fail(set_error(OMR_ERR_OUT_OF_MEMORY, "omr_ctx_create: key buffers"));
   const double ninv2 = centred(h_powmod(N2, Q2 - 2, Q2), Q2);
@@ -852,33 +875,40 @@ extern "C" omr_status omr_ctx_create(const omr_detection_key_view *key, int devi
   if ((st = convert_keys_cmux(key->bsk2, BSK2_ELEMS / N2, c->bsk2, ninv2, c->tb.tw2c, c->stream)) != OMR_OK)
     return fail(st);
   if ((st = convert_keys_dd<2>(key->bsk2, BSK2_ELEMS / N2, c->bsk2f, c->stream)) != OMR_OK) return fail(st);
+  if ((st = convert_keys_dd<2>(key->trace_key, TK_ELEMS / N2, c->tkf, c->stream)) != OMR_OK) return fail(st);
   {  // kappa_r per key row (the a priori bound's key constants) and the guard's margin words
-    const size_t rows1 = BSK1_ELEMS / 2 / Fft512::N, rows2 = BSK2_ELEMS / Fft1024::n;
+    const size_t rows1 = BSK1_ELEMS / 2 / Fft512::N, rows2 = BSK2_ELEMS / Fft1024::n, rowst = TK_ELEMS / Fft1024::n;
     DevBufHost<double> km;
     if (hipMalloc(&c->margin, GUARD_WORDS * sizeof(unsigned long long)) != hipSuccess ||
-        hipMalloc(&km.p, (rows1 + rows2) * sizeof(double)) != hipSuccess)
+        hipMalloc(&km.p, (rows1 + rows2 + rowst) * sizeof(double)) != hipSuccess)
       return fail(set_error(OMR_ERR_OUT_OF_MEMORY, "omr_ctx_create: margin words"));
     const bool ok = hipMemsetAsync(c->margin, 0, GUARD_WORDS * sizeof(unsigned long long), c->stream) == hipSuccess;
     if (ok) {
       row_max_abs_kernel<<<(unsigned)rows1, 256, 0, c->stream>>>(c->bsk1f, Fft512::N, km.p);
       row_max_abs_kernel<<<(unsigned)rows2, 256, 0, c->stream>>>(c->bsk2f, Fft1024::n, km.p + rows1);
+      row_max_abs_kernel<<<(unsigned)rowst, 256, 0, c->stream>>>(c->tkf, Fft1024::n, km.p + rows1 + rows2);
     }
-    std::vector<double> k1(rows1), k2(rows2);
+    std::vector<double> k1(rows1), k2(rows2), kt(rowst);
     if (!ok || hipGetLastError() != hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess ||
         hipMemcpy(k1.data(), km.p, rows1 * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess ||
-        hipMemcpy(k2.data(), km.p + rows1, rows2 * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess)
+        hipMemcpy(k2.data(), km.p + rows1, rows2 * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(kt.data(), km.p + rows1 + rows2, rowst * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess)
       return fail(set_error(OMR_ERR_DEVICE, "omr_ctx_create: key spectrum maxima"));
     c->kappa[0] = *std::max_element(k1.begin(), k1.end());
     c->kappa[1] = *std::max_element(k2.begin(), k2.end());
     c->apriori[0] = apriori_bound(1, k1);
     c->apriori[1] = apriori_bound(2, k2);
     c->apriori_y = apriori_bound(3, k2);
+    c->apriori_t = apriori_bound(4, kt);
+    c->trace_fft = c->apriori_t < 0.5;
     // the exactness contract: a level whose bound does not prove every rounding exact is guarded
     // on every launch and checked against 1 - E (omr_ctx_exactness)
     for (int l = 0; l < 2; ++l) {
       c->guard_auto[l] = !(c->apriori[l] < 0.5);
       c->thr[l] = 1.0 - c->apriori[l];
     }
+    // the fused FFT trace shares level 2's guard word and threshold
+    if (c->trace_fft) c->thr[1] = 1.0 - std::max(c->apriori[1], c->apriori_t);
   }
   if ((st = convert_keys<2, uint64_t, double>(key->trace_key, TK_ELEMS / N2, c->tk, 1.0, c->tb.tw2,
                                               c->stream)) != OMR_OK)
@@ -909,6 +939,7 @@ extern "C" void omr_ctx_destroy(omr_ctx *c) {
   dev_free(c->fft1);
   dev_free(c->bsk2);
   dev_free(c->bsk2f);
+  dev_free(c->tkf);
   dev_free(c->fft2);
   dev_free(c->tk);
   dev_free(c->kskb);
@@ -1056,16 +1087,18 @@ omr_status launch_dual(omr_ctx *c, size_t B1, const uint16_t *ca1, const uint16_
   HIP_TRY(hipMemsetAsync(c->dual_ctl, 0, DUAL_CTL_WORDS * sizeof(unsigned), st));
   const size_t nrot = B1 * CLUES;
   const unsigned n1 = (unsigned)((nrot + BR1F_WPG - 1) / BR1F_WPG), n2 = (unsigned)B2;
-  dual_kernel<<<n1 + n2, 256, 0, st>>>(ca1, cb1, c->bsk1f, c->ext, nrot, n1, c->lwe_int, c->bsk2f, c->fft2, c->tk,
-                                       out2, n2, c->tb, c->dual_ctl);
+  dual_kernel<<<n1 + n2, 256, 0, st>>>(ca1, cb1, c->bsk1f, c->ext, nrot, n1, c->lwe_int, c->bsk2f, c->fft2, out2, n2,
+                                       c->tb, c->dual_ctl);
+  HIP_TRY(hipGetLastError());
+  trace_fft_kernel<<<n2, Fft1024::T, 0, st>>>(out2, c->tkf, c->fft2, c->tb);
   HIP_TRY(hipGetLastError());
   return OMR_OK;
 }
 
 // Detect D messages of device buffers on st, in chunks of c->batch: per chunk br1f (7 rotations
 // per message) -> sum7 -> key switch -> br2 + trace. Stage events per chunk: [0] br1 start,
-// [1] br1 end, [2] key switch end, [3] level-2 rotation end, [4] trace end ([3] = [4] when the
-// throughput kernel fuses the trace, timing mode 1).
+// [1] br1 end, [2] key switch end, [3] level-2 rotation end, [4] trace end (the trace is its own
+// launch on both kernel families since round 5: trace_fft_kernel / trace_x_kernel).
 omr_status detect_device(omr_ctx *c, const uint16_t *ca, const uint16_t *cb, size_t D,
                          uint64_t *out, hipStream_t st) {
   omr_status s;
@@ -1090,7 +1123,7 @@ omr_status detect_device(omr_ctx *c, const uint16_t *ca, const uint16_t *cb, siz
   // (the dual launch that carries it), [2] after its key switch, [3] = [4] after the launch that
   // carries its level 2 -- the two levels overlap, so the split is of launches, not of levels.
   const size_t per = (D + c->dual_chunks - 1) / c->dual_chunks;
-  if (c->dual && !split && !guarded(c, 0) && !guarded(c, 1) && D >= 2 && !latency_path(c, std::min(per, c->batch))) {
+  if (c->dual && c->trace_fft && !split && !guarded(c, 0) && !guarded(c, 1) && D >= 2 && !latency_path(c, std::min(per, c->batch))) {
     const size_t B = std::min(per, c->batch), nch = (D + B - 1) / B;
     if (c->timing) {
       while (c->events.size() < nch * EV_PER_CHUNK) {
@@ -1146,7 +1179,6 @@ omr_status detect_device(omr_ctx *c, const uint16_t *ca, const uint16_t *cb, siz
     if ((s = launch_br2(c, (size_t)B, c->lwe_int, out + off * 2 * N2, 0, st, split, ev ? ev[3] : nullptr)) != OMR_OK)
       return s;
     if (ev) HIP_TRY(hipEventRecord(ev[4], st));
-    if (ev && !split && !latency_path(c, (size_t)B)) c->timed_split = false;
   }
   return scratch_release(c, st);
 }

@@ -35,29 +35,24 @@ struct Digits2 {
     return (k < 3 ? field<0>(pk, k) : field<1>(pk, k - 3)) - 64;
   }
 };
-// Trace basis (q2, 2, None): 25 digits in [-2, 2], 3 bits each (value + 2), 10 per dword.
+// Trace basis (q2, 2, None): 25 balanced base-4 digits (24 in [-2, 1], the top one in [-2, 3]).
 struct DigitsTrace {
-  static constexpr int DW = 3;
+  static constexpr int DW = 2;
+  static_assert(DT == 25, "closed form written for the trace basis");
+  // Closed form of the recursive balanced base-4 decomposition (d = y - 4 floor(y / 4 + 1/2), 24
+  // times, then the rest; round 5): y' = v + 2 (1 + 4 + ... + 4^23) has field k (bits 2k, 2k + 1)
+  // = d_k + 2 for k < 24 and y' >> 48 = d_24. Y = y' + 1.5 * 2^52 is exact (|v| < 2^49) and the low
+  // 51 bits of its mantissa are y' in two's complement, so the words are Y's two dwords, each field
+  // XORed with 2 (a two's-complement 2-bit digit: one v_bfe_i32): 1 FP64 add and 2 XORs per
+  // coefficient instead of 24 floor / fma / conversion rounds (tests/test_lvl1_offset_model.py).
   __device__ static __forceinline__ void pack(double v, uint32_t (&pk)[DW]) {
-    double y = v;
-    pk[0] = pk[1] = pk[2] = 0;
-#pragma unroll
-    for (int k = 0; k < DT; ++k) {
-      double d;
-      if (k < DT - 1) {
-        const double c = floor(__fma_rn(y, 0.25, 0.5));
-        d = __fma_rn(-c, 4.0, y);
-        y = c;
-      } else {
-        d = y;
-      }
-      pk[k / 10] |= (uint32_t)((int)d + 2) << (3 * (k % 10));
-    }
+    const uint64_t b = __builtin_bit_cast(uint64_t, v + (187649984473770.0 + 6755399441055744.0));
+    pk[0] = (uint32_t)b ^ 0xAAAAAAAAu;      // digits 0..15
+    pk[1] = (uint32_t)(b >> 32) ^ 0xAAAAu;  // digits 16..23 in bits 0..15, d_24 in bits 16..18
   }
   __device__ static __forceinline__ int get_int(const uint32_t (&pk)[DW], int k) {
-    const int wi = k / 10;
-    const uint32_t w = wi == 0 ? pk[0] : (wi == 1 ? pk[1] : pk[2]);
-    return (int)((w >> (3 * (k - 10 * wi))) & 7u) - 2;
+    const uint32_t w = k < 16 ? pk[0] : pk[1];
+    return (int)__builtin_amdgcn_sbfe(w, k < 16 ? 2 * k : 2 * (k - 16), k == DT - 1 ? 3 : 2);
   }
   __device__ static __forceinline__ double get(const uint32_t (&pk)[DW], int k) { return (double)get_int(pk, k); }
 };

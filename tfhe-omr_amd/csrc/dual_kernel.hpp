@@ -11,8 +11,8 @@
 // CU / SH / SE fields; the placement decides speed only), then takes the next item of that role's
 // queue, or of the other role's when that one is empty -- the grid has exactly one workgroup per
 // item, so every workgroup gets one. The bodies are br1f_body / br2f_body unchanged (mode 0:
-// extracted LWEs; the NttRlwe output with the trace fused), so the outputs are bit-identical to
-// the sequential launches.
+// extracted LWEs; the coefficient-domain rotation, traced by the launch after), so the outputs
+// are bit-identical to the sequential launches.
 // ctl: [0] level-1 queue, [1] level-2 queue, [2 + key] this CU's active workgroups (level 1 in the
 // low 16 bits, level 2 in the high 16); zeroed before every launch.
 #pragma once
@@ -35,8 +35,8 @@ __device__ __forceinline__ unsigned dual_cu_key() {
 __global__ __launch_bounds__(256, 2) void dual_kernel(
     const uint16_t *__restrict__ clue_a, const uint16_t *__restrict__ clue_b, const double2 *__restrict__ bsk1f,
     uint32_t *__restrict__ ext, size_t nrot, unsigned n1, const uint32_t *__restrict__ lwe_int,
-    const double2 *__restrict__ bsk2f, const double2 *__restrict__ twg, const double *__restrict__ tk,
-    uint64_t *__restrict__ out, unsigned n2, DeviceTables tb, unsigned *ctl) {
+    const double2 *__restrict__ bsk2f, const double2 *__restrict__ twg, uint64_t *__restrict__ out, unsigned n2,
+    DeviceTables tb, unsigned *ctl) {
   static_assert(64 * BR1F_WPG == Fft1024::T, "both roles run 256-thread workgroups");
   static_assert(BR1_LDS_XCH == 0 && BR2_LDS_X == 0, "the pool's 8 KB alignment serves br1f_digits");
   __shared__ __attribute__((aligned(8192))) double2 pool[DUAL_LDS_BYTES / sizeof(double2)];
@@ -66,7 +66,7 @@ __global__ __launch_bounds__(256, 2) void dual_kernel(
     br1f_body<false>(clue_a, clue_b, nullptr, nullptr, bsk1f, tb, ext, nullptr, 0, nrot, nullptr,
                      reinterpret_cast<char *>(pool), item);
   else
-    br2f_body<false>(lwe_int, bsk2f, twg, tk, tb, out, 0, nullptr, pool, item);
+    br2f_body<false>(lwe_int, bsk2f, twg, tb, out, nullptr, pool, item);
   if (threadIdx.x == 0) atomicSub(cnt, role ? 0x10000u : 1u);
 }
 

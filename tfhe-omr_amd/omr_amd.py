@@ -505,8 +505,8 @@ class Detector:
         return out.view(np.complex128)
 
     def enable_timing(self, mode: int = 1):
-        """0 off; 1 stage events around the production kernels (the throughput path fuses the
-        trace into level 2); 2 the reference's split (trace as its own launch)."""
+        """0 off; 1 stage events around the production kernels; 2 the reference's split (the
+        trace as its own launch: the throughput path's production form since round 5)."""
         _check(lib().omr_ctx_enable_timing(self._h, int(mode)), "omr_ctx_enable_timing")
 
     def last_timing(self) -> dict:
