@@ -55,10 +55,9 @@ typedef enum {
   OMR_ERR_DEVICE = 2,
   OMR_ERR_OUT_OF_MEMORY = 3,
   OMR_ERR_NOT_INVERTIBLE = 4, /* OmrError::InvertibleMatrix, error.rs:5-8 */
-  /* A level-1 FFT external product of a detect call could not be certified exact: the key's a
-   * priori bound E1 is >= 0.5 and the call's observed rounding margin reached 1 - E1 (see
-   * omr_ctx_exactness). The outputs of that call are not guaranteed; the reference's products are
-   * exact for every key (concrete-ntt, omr_core/Cargo.toml:38-45). */
+  /* Reserved (kept for ABI stability): up to round 5 an uncertified level-1 FFT product was reported
+   * with this code; such a launch is now re-run on the exact NTT (omr_ctx_exactness), so no call
+   * returns it. */
   OMR_ERR_INEXACT = 5
 } omr_status;
 
@@ -200,12 +199,18 @@ omr_status omr_ctx_rounding_margin(omr_ctx *ctx, double observed[2], double apri
  * such launch the observed margin m of that launch is compared with 1 - E on the device:
  *  - level 2: a launch with m >= 1 - E2 is re-run on the exact modular NTT (the latency family's
  *    br2l_kernel + trace), in the same stream order, so its outputs are exact;
- *  - level 1: a launch with m >= 1 - E1 marks the context; the host entry points, omr_ctx_check and
- *    the next detect call report it as OMR_ERR_INEXACT (and clear it).
+ *  - level 1: a launch with m >= 1 - E1 is re-run on the exact modular NTT (br1n_fallback_kernel,
+ *    br1_ntt.hpp) in the same stream order, so its outputs are exact (round 5; before, such a launch
+ *    was reported as OMR_ERR_INEXACT, a code no call returns any more).
  * guarded[l] != 0 when level l + 1 is guarded on every launch (automatically or by the user);
  * breaches[l] counts the launches of level l + 1 whose margin reached the threshold. Any pointer
  * may be NULL. Reading breaches synchronises the device. */
 omr_status omr_ctx_exactness(omr_ctx *ctx, int guarded[2], uint64_t breaches[2]);
+/* Level 1 on the exact modular NTT for every launch of the context (br1n_kernel: the reference's
+ * own arithmetic, concrete-ntt in BlindRotationKey::blind_rotate, detector.rs:553-557), instead of the
+ * FFT kernels; enable = 0 restores them. Outputs are bit-identical either way -- a cross-check of
+ * the FFT path at any size, about 3x slower at level 1. */
+omr_status omr_ctx_set_exact_level1(omr_ctx *ctx, int enable);
 /* Diagnostics: `count` stored key-spectrum values (complex, re/im pairs) starting at value `first`
  * of level 1 (BSK1, [512][8][2][512], /512) or level 2 (BSK2 limbs, [670][12][2][2][1024], /1024),
  * in the kernels' storage order (register-major slots). */

@@ -32,7 +32,7 @@ pub mod ffi {
     pub const OMR_ERR_DEVICE: OmrStatus = 2;
     pub const OMR_ERR_OUT_OF_MEMORY: OmrStatus = 3;
     pub const OMR_ERR_NOT_INVERTIBLE: OmrStatus = 4;
-    /// a level-1 FFT product of a detect call could not be certified exact (omr_ctx_exactness)
+    /// reserved: no call returns it since level-1 breaches are re-run on the exact NTT
     pub const OMR_ERR_INEXACT: OmrStatus = 5;
 
     pub const OMR_N0: usize = 512;
@@ -131,6 +131,7 @@ pub mod ffi {
         pub fn omr_detect_kernels() -> *const c_char;
         pub fn omr_ctx_set_batch(ctx: *mut OmrCtx, batch: usize) -> OmrStatus;
         pub fn omr_ctx_set_latency_threshold(ctx: *mut OmrCtx, max_messages: usize) -> OmrStatus;
+        pub fn omr_ctx_set_exact_level1(ctx: *mut OmrCtx, enable: c_int) -> OmrStatus;
         pub fn omr_ctx_set_encode_chunks(ctx: *mut OmrCtx, max_chunks: usize) -> OmrStatus;
         pub fn omr_detect_batch(ctx: *mut OmrCtx, clue_a: *const u16, clue_b: *const u16, d: usize,
                                 out: *mut u64) -> OmrStatus;
@@ -496,7 +497,7 @@ impl GpuDetector {
 
     /// The exactness contract (`omr_ctx_exactness`): (guarded on every launch, breaching launches)
     /// per level. A level whose a priori bound is >= 0.5 is guarded automatically; a level-2 breach
-    /// was re-run on the exact NTT, a level-1 breach surfaced as `OMR_ERR_INEXACT`.
+    /// (either level) was re-run on the exact NTT.
     pub fn exactness(&self) -> Result<([bool; 2], [u64; 2]), OmrError> {
         let (mut g, mut b) = ([0 as c_int; 2], [0u64; 2]);
         check(unsafe { omr_ctx_exactness(self.ctx, g.as_mut_ptr(), b.as_mut_ptr()) })?;
@@ -506,6 +507,12 @@ impl GpuDetector {
     /// Chunks of at most `max_messages` messages run the latency kernels (0 = never).
     pub fn set_latency_threshold(&self, max_messages: usize) -> Result<(), OmrError> {
         check(unsafe { omr_ctx_set_latency_threshold(self.ctx, max_messages) })
+    }
+
+    /// Level 1 on the exact modular NTT for every launch (`omr_ctx_set_exact_level1`): the
+    /// reference's arithmetic, bit-identical outputs, slower.
+    pub fn set_exact_level1(&self, enable: bool) -> Result<(), OmrError> {
+        check(unsafe { omr_ctx_set_exact_level1(self.ctx, enable as c_int) })
     }
 }
 

@@ -12,16 +12,32 @@ detect path (any canonical residues are), so the GPU output is checked against t
 """
 import numpy as np
 
+Q1 = 134215681
 Q2 = 1125899906826241
 LIMB_MAX = (1 << 24) - 1
+H1 = (Q1 - 1) // 2
 
 
-def aligned_row(n=1024):
-    """A coefficient-domain row (2n centred values) whose folded spectrum peaks at point 0."""
+def aligned_row(n=1024, peak=LIMB_MAX):
+    """A coefficient-domain row (2n centred values of magnitude `peak`) whose folded spectrum peaks
+    at point 0."""
     phi = np.pi * np.arange(n) / (2 * n)
-    re = np.where(np.cos(phi) >= 0, LIMB_MAX, -LIMB_MAX)
-    im = np.where(np.sin(phi) >= 0, -LIMB_MAX, LIMB_MAX)  # Re(i v e^{i phi}) = -v sin(phi)
+    re = np.where(np.cos(phi) >= 0, peak, -peak)
+    im = np.where(np.sin(phi) >= 0, -peak, peak)  # Re(i v e^{i phi}) = -v sin(phi)
     return np.concatenate([re, im]).astype(np.int64)
+
+
+def high_kappa_bsk1(bsk1, steps=(0, 1, 2, 3)):
+    """Level 1 the same way (round 5): a copy of bsk1 (u32 [512][8][2][1024]) with every row and
+    output of `steps` set to the aligned row of peak (q1 - 1) / 2, the largest centred residue: the
+    folded 512-point spectrum then peaks at 4 / pi * 512 * (q1 - 1) / 2, about 24x a uniform row's,
+    which puts E1 above 1."""
+    out = np.array(bsk1, dtype=np.uint32, copy=True).reshape(512, 8, 2, 1024)
+    row = aligned_row(512, H1)
+    canon = np.where(row < 0, row + Q1, row).astype(np.uint32)
+    for i in steps:
+        out[i, :, :, :] = canon[None, None, :]
+    return out.reshape(np.shape(bsk1))
 
 
 def high_kappa_bsk2(bsk2, steps=(0, 1, 2, 3)):

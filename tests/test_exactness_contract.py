@@ -38,6 +38,10 @@ def test_apriori_bound_uniform_key_below_half_and_crafted_key_above():
     assert c2 >= 1.0, f"crafted key E2 = {c2}: the guard must be on and every launch re-run exactly"
     # the crafted limb peak: 4 / pi of the limb bound (sum of |cos| + |sin| over the quarter turn)
     assert abs(ck2 / CK.LIMB_MAX - 4 / np.pi) < 1e-3
+    crafted1 = types.SimpleNamespace(bsk1=CK.high_kappa_bsk1(dk.bsk1), bsk2=dk.bsk2)
+    d1, d2, dk1, dk2 = FB.apriori_bounds(crafted1)
+    assert d2 == e2 and dk2 == k2, "level 2 untouched"
+    assert dk1 > 5 * k1 and d1 >= 1.0, (d1, dk1, k1)
 
 
 def test_header_declares_the_contract():

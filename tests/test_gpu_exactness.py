@@ -105,6 +105,28 @@ def test_latency_family_exact_ntt_matches_full_launch(full):
     assert not bad, f"{int(diff.sum())} messages differ between the FFT and NTT level 2, e.g. {bad}"
 
 
+def test_exact_level1_ntt_matches_full_launch(full):
+    """All 65,536 outputs with level 1 on the exact modular NTT (omr_ctx_set_exact_level1:
+    br1n_kernel, the reference's arithmetic for all 458,752 rotations) equal the production FFT
+    launch's: the full-size check of the level-1 FFT that the latency family cannot give (both
+    families share the level-1 FFT)."""
+    import time
+    import torch
+    det, d_ca, d_cb, want, mask = full
+    got = torch.empty_like(want)
+    det.set_exact_level1(True)
+    try:
+        t = time.perf_counter()
+        det.detect_batch_device(d_ca.data_ptr(), d_cb.data_ptr(), D_FULL, got.data_ptr(), None)
+        det.check()
+        print(f"\nexact-NTT level 1 + FFT level 2 over {D_FULL} messages: {time.perf_counter() - t:.2f} s")
+    finally:
+        det.set_exact_level1(False)
+    diff = (got != want).reshape(D_FULL, -1).any(dim=1)
+    bad = torch.nonzero(diff).flatten()[:8].tolist()
+    assert not bad, f"{int(diff.sum())} messages differ between the FFT and NTT level 1, e.g. {bad}"
+
+
 # ---- double-double key spectra ------------------------------------------------------------------
 def _tree_fft_ld(z, L):
     """The natural-order tree transform of key_spectra.hpp in numpy long double (64-bit mantissa)."""
@@ -248,6 +270,78 @@ def test_high_kappa_key_guarded_and_oracle_exact():
         assert np.array_equal(got, ref), "guarded high-kappa detect differs from the oracle"
         assert np.array_equal(got_split, ref[:40]), "split-trace path differs from the oracle"
         assert np.array_equal(det.blind_rotate_level2(lwe), ref_rot), "level-2 rotation entry differs"
+        det.check()
+    finally:
+        det.close()
+
+
+def test_high_kappa_level1_key_rerun_exact():
+    """A key whose level-1 a priori bound E1 is >= 1 (tests/crafted_keys.py: aligned maximal BSK1
+    rows on four steps): the context guards level 1 on every launch without being asked, every such
+    launch breaches the threshold 1 - E1 <= 0 and is re-run on the exact NTT (br1n_fallback_kernel),
+    and the outputs equal the oracle's on both kernel families and through the level-1 entries."""
+    import crafted_keys as CK
+    import oracle_lib as O
+    _, _, dk = PL.keys()
+    ck = A.DetectionKey(CK.high_kappa_bsk1(dk.bsk1), dk.ksk, dk.bsk2, dk.trace_key)
+    det = A.Detector(ck)
+    try:
+        m = det.rounding_margin()
+        assert m["apriori"][1] < 0.5 <= 1.0 <= m["apriori"][0], m
+        from fft_bound import apriori_bounds
+        e1, _, _, _ = apriori_bounds(ck)
+        assert abs(m["apriori"][0] - e1) < 1e-9 * e1
+        assert det.exactness() == {"guarded": [True, False], "breaches": [0, 0]}
+        mask = np.arange(72) % 9 == 0
+        ca, cb = PL.mixed_clues(mask, seed=78)
+        det.set_latency_threshold(0)  # throughput kernels: br1f_guard_kernel + the fallback
+        got = det.detect_batch(ca, cb)
+        ex = det.exactness()
+        assert ex["guarded"] == [True, False] and ex["breaches"][0] >= 1 and ex["breaches"][1] == 0, ex
+        det.set_latency_threshold(64)  # latency kernels: br1l_guard_kernel + the fallback
+        got_lat = det.detect_batch(ca[:5], cb[:5])
+        assert det.exactness()["breaches"][0] > ex["breaches"][0]
+        orc = O.OracleDetector(ck.bsk1, ck.ksk, ck.bsk2, ck.trace_key)
+        try:
+            ref = orc.detect_batch(ca, cb)
+            lwe = np.stack([orc.first_level(ca[i], cb[i]) for i in range(3)])
+        finally:
+            orc.close()
+        assert np.array_equal(got, ref), "guarded high-kappa level-1 detect differs from the oracle"
+        assert np.array_equal(got_lat, ref[:5]), "latency family differs from the oracle"
+        assert np.array_equal(det.first_level(ca[:3], cb[:3]), lwe), "level-1 stage entry differs"
+        det.check()
+    finally:
+        det.close()
+
+
+def test_exact_level1_small_matches_oracle():
+    """omr_ctx_set_exact_level1 at oracle sizes: both detect families and the mode-1 rotation entry
+    (explicit LWEs -> full RLWE) equal the oracle with level 1 on br1n_kernel."""
+    import oracle_lib as O
+    _, _, dk = PL.keys()
+    det = A.Detector(dk)
+    try:
+        det.set_exact_level1(True)
+        mask = np.arange(70) % 7 == 0
+        ca, cb = PL.mixed_clues(mask, seed=79)
+        det.set_latency_threshold(0)
+        got = det.detect_batch(ca, cb)
+        det.set_latency_threshold(64)
+        got_lat = det.detect_batch(ca[:3], cb[:3])
+        rng = np.random.default_rng(80)
+        la = rng.integers(0, 2048, size=(5, 512), dtype=np.uint16)
+        lb = rng.integers(0, 2048, size=5, dtype=np.uint16)
+        rot = det.blind_rotate_level1(la, lb)
+        det.set_exact_level1(False)
+        assert np.array_equal(det.blind_rotate_level1(la, lb), rot), "FFT vs NTT level-1 rotation entry"
+        orc = O.OracleDetector(dk.bsk1, dk.ksk, dk.bsk2, dk.trace_key)
+        try:
+            ref = orc.detect_batch(ca, cb)
+        finally:
+            orc.close()
+        assert np.array_equal(got, ref), "exact-NTT level 1 (throughput family) differs from the oracle"
+        assert np.array_equal(got_lat, ref[:3]), "exact-NTT level 1 (latency family) differs from the oracle"
         det.check()
     finally:
         det.close()

@@ -16,6 +16,7 @@
 #include <string>
 #include <vector>
 
+#include "br1_ntt.hpp"
 #include "br2_fft.hpp"
 #include "detect_kernels.hpp"
 #include "dual_kernel.hpp"
@@ -283,6 +284,7 @@ struct omr_ctx {
   hipStream_t stream = nullptr;
   double2 *bsk1f = nullptr;  // level-1 FFT-domain keys [512][8][2][512] complex, x 1/512
   double2 *bsk1l = nullptr;  // the same in br1l_kernel's layout [512][8 slot][8 row][2][64 lane]
+  double *bsk1n = nullptr;   // BSK1 in the NTT domain x 1/1024 [512][8][2][1024] (br1_ntt.hpp: level 1's exact path)
   double2 *fft1 = nullptr;   // level-1 FFT twiddles
   double *bsk2 = nullptr, *tk = nullptr;  // BSK2 NTT domain (latency kernels), trace key
   double2 *bsk2f = nullptr;                // BSK2 as FFT-domain 25-bit limbs (br2f_kernel), x 1/1024
@@ -318,6 +320,8 @@ struct omr_ctx {
   // the breach counts); kappa: largest stored key spectrum magnitude per level; apriori: the bound it
   // gives (apriori_bound); thr = 1 - apriori, the certificate threshold of one launch
   bool guard = false, guard_auto[2] = {false, false};
+  // omr_ctx_set_exact_level1: every level-1 launch on the exact modular NTT (br1n_kernel)
+  bool exact1 = false;
   unsigned long long *margin = nullptr;
   double kappa[2] = {0.0, 0.0}, apriori[2] = {0.0, 0.0}, thr[2] = {1.0, 1.0};
   // the fused trace on the FFT (br2f_trace) when its a priori bound (apriori_bound level 4) is below
@@ -530,21 +534,14 @@ bool latency_path(const omr_ctx *c, size_t n) { return n <= c->latency_max; }
 // reports (and clears) an error whose copy has landed: callers sync the stream first for a
 // definitive answer (omr_ctx_check, the host entry points), or call it before enqueueing new work
 // (the device entry points) so a failed earlier call is never attributed to a later one.
-// The same word carries GUARD_ERR_INEXACT: a guarded level-1 launch whose rounding margin reached
-// the certificate threshold (guard_fold_kernel), reported as OMR_ERR_INEXACT.
 omr_status take_handoff_error(omr_ctx *c) {
   if (!c->x_err_host || !__atomic_load_n(c->x_err_host, __ATOMIC_ACQUIRE)) return OMR_OK;
   HIP_TRY(hipDeviceSynchronize());  // no launch may still be copying the flag
-  const int bits = __atomic_exchange_n(c->x_err_host, 0, __ATOMIC_ACQ_REL);
+  (void)__atomic_exchange_n(c->x_err_host, 0, __ATOMIC_ACQ_REL);
   HIP_TRY(hipMemset(c->x_err, 0, sizeof(int)));
-  if (bits & GUARD_ERR_HANDOFF)
-    return set_error(OMR_ERR_DEVICE,
-                     "level-2 two-CU hand-off timed out: the output of an earlier detect call on this "
-                     "context is invalid");
-  return set_error(OMR_ERR_INEXACT,
-                   "a level-1 FFT external product of an earlier detect call on this context could not "
-                   "be certified exact (key a priori bound E1 >= 0.5 and margin >= 1 - E1): its output "
-                   "is not guaranteed");
+  return set_error(OMR_ERR_DEVICE,
+                   "level-2 two-CU hand-off timed out: the output of an earlier detect call on this "
+                   "context is invalid");
 }
 
 // Zero the per-launch guard word of `level` before a guarded launch.
@@ -552,13 +549,11 @@ omr_status guard_begin(omr_ctx *c, int level, hipStream_t st) {
   HIP_TRY(hipMemsetAsync(c->margin + 2 + level, 0, sizeof(unsigned long long), st));
   return OMR_OK;
 }
-// After a guarded launch (and, for level 2, its conditional exact re-run): fold the launch's margin
-// into the cumulative word, count a breach, and (level 1) raise the context's error word, which is
-// copied to the pinned host word like the hand-off timeout.
+// After a guarded launch and its conditional exact re-run: fold the launch's margin into the
+// cumulative word and count a breach.
 omr_status guard_end(omr_ctx *c, int level, hipStream_t st) {
-  guard_fold_kernel<<<1, 64, 0, st>>>(c->margin, level, c->thr[level], c->x_err);
+  guard_fold_kernel<<<1, 64, 0, st>>>(c->margin, level, c->thr[level]);
   HIP_TRY(hipGetLastError());
-  if (level == 0) HIP_TRY(hipMemcpyAsync(c->x_err_host, c->x_err, sizeof(int), hipMemcpyDeviceToHost, st));
   return OMR_OK;
 }
 
@@ -582,6 +577,11 @@ omr_status launch_ks(omr_ctx *c, int B, uint32_t *out, hipStream_t st) {
 omr_status launch_br1(omr_ctx *c, size_t n, const uint16_t *ca, const uint16_t *cb,
                       const uint16_t *la, const uint16_t *lb, uint32_t *ext, uint64_t *rlwe, int mode,
                       hipStream_t st, size_t msgs) {
+  if (c->exact1) {  // the reference's arithmetic for every rotation (omr_ctx_set_exact_level1)
+    br1n_kernel<<<(unsigned)n, 64, 0, st>>>(ca, cb, la, lb, c->bsk1n, c->tb, ext, rlwe, mode, n);
+    HIP_TRY(hipGetLastError());
+    return OMR_OK;
+  }
   const unsigned g1 = (unsigned)((n + BR1F_WPG - 1) / BR1F_WPG);
   const bool g = guarded(c, 0);
   omr_status s;
@@ -599,7 +599,13 @@ omr_status launch_br1(omr_ctx *c, size_t n, const uint16_t *ca, const uint16_t *
     br1f_kernel<<<g1, 64 * BR1F_WPG, 0, st>>>(ca, cb, la, lb, c->bsk1f, c->tb, ext, rlwe, mode, n);
   }
   HIP_TRY(hipGetLastError());
-  return g ? guard_end(c, 0, st) : OMR_OK;
+  if (!g) return OMR_OK;
+  // the exactness contract: a guarded launch whose margin reached 1 - E1 is recomputed on the exact
+  // NTT in the same stream order (every workgroup leaves at once otherwise)
+  br1n_fallback_kernel<<<(unsigned)n, 64, 0, st>>>(ca, cb, la, lb, c->bsk1n, c->tb, ext, rlwe, mode, n,
+                                                   c->margin + 2, c->thr[0]);
+  HIP_TRY(hipGetLastError());
+  return guard_end(c, 0, st);
 }
 
 // br2x_kernel over 2 n workgroups as a cooperative launch (co-residency guaranteed, or the launch
@@ -794,7 +800,7 @@ extern "C" omr_status omr_ctx_create(const omr_detection_key_view *key, int devi
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&c->scratch_free, hipEventDisableTiming) != hipSuccess)
     return fail(set_error(OMR_ERR_DEVICE, "hipStreamCreate / hipEventCreate failed"));
-  // the context's error word (hand-off timeout, uncertified level-1 product) and its pinned copy
+  // the context's error word (a two-CU hand-off timeout) and its pinned copy
   if (hipMalloc(&c->x_err, sizeof(int)) != hipSuccess || hipMemset(c->x_err, 0, sizeof(int)) != hipSuccess ||
       hipHostMalloc((void **)&c->x_err_host, sizeof(int), hipHostMallocDefault) != hipSuccess)
     return fail(set_error(OMR_ERR_OUT_OF_MEMORY, "omr_ctx_create: error word"));
@@ -860,6 +866,7 @@ extern "C" omr_status omr_ctx_create(const omr_detection_key_view *key, int devi
   // keys
   if (hipMalloc(&c->bsk1f, BSK1_ELEMS / 2 * sizeof(double2)) != hipSuccess ||
       hipMalloc(&c->bsk1l, BSK1_ELEMS / 2 * sizeof(double2)) != hipSuccess ||
+      hipMalloc(&c->bsk1n, BSK1_ELEMS * sizeof(double)) != hipSuccess ||
       hipMalloc(&c->bsk2, BSK2_ELEMS * sizeof(double)) != hipSuccess ||
       hipMalloc(&c->bsk2f, BSK2_ELEMS * sizeof(double2)) != hipSuccess ||
       hipMalloc(&c->tk, TK_ELEMS * sizeof(double)) != hipSuccess ||
@@ -872,6 +879,10 @@ extern "C" omr_status omr_ctx_create(const omr_detection_key_view *key, int devi
   bsk1_latency_layout_kernel<<<(unsigned)(BSK1_ELEMS / 2 / 256), 256, 0, c->stream>>>(c->bsk1f, c->bsk1l,
                                                                                      BSK1_ELEMS / 2);
   if (hipGetLastError() != hipSuccess) return fail(set_error(OMR_ERR_DEVICE, "omr_ctx_create: BSK1 layout"));
+  const double ninv1 = centred(h_powmod(N1, Q1 - 2, Q1), Q1);
+  if ((st = convert_keys<1, uint32_t, double>(key->bsk1, BSK1_ELEMS / N1, c->bsk1n, ninv1, c->tb.tw1,
+                                              c->stream)) != OMR_OK)
+    return fail(st);
   if ((st = convert_keys_cmux(key->bsk2, BSK2_ELEMS / N2, c->bsk2, ninv2, c->tb.tw2c, c->stream)) != OMR_OK)
     return fail(st);
   if ((st = convert_keys_dd<2>(key->bsk2, BSK2_ELEMS / N2, c->bsk2f, c->stream)) != OMR_OK) return fail(st);
@@ -936,6 +947,7 @@ extern "C" void omr_ctx_destroy(omr_ctx *c) {
   if (c->scratch_stream) (void)hipEventSynchronize(c->scratch_free);
   dev_free(c->bsk1f);
   dev_free(c->bsk1l);
+  dev_free(c->bsk1n);
   dev_free(c->fft1);
   dev_free(c->bsk2);
   dev_free(c->bsk2f);
@@ -1005,6 +1017,13 @@ extern "C" omr_status omr_ctx_set_rounding_guard(omr_ctx *c, int enable) {
   if (!c) return set_error(OMR_ERR_INVALID_ARGUMENT, "omr_ctx_set_rounding_guard: NULL ctx");
   std::lock_guard<std::mutex> lk(c->mu);
   c->guard = enable != 0;
+  return OMR_OK;
+}
+
+extern "C" omr_status omr_ctx_set_exact_level1(omr_ctx *c, int enable) {
+  if (!c) return set_error(OMR_ERR_INVALID_ARGUMENT, "omr_ctx_set_exact_level1: NULL ctx");
+  std::lock_guard<std::mutex> lk(c->mu);
+  c->exact1 = enable != 0;
   return OMR_OK;
 }
 
@@ -1123,7 +1142,7 @@ omr_status detect_device(omr_ctx *c, const uint16_t *ca, const uint16_t *cb, siz
   // (the dual launch that carries it), [2] after its key switch, [3] = [4] after the launch that
   // carries its level 2 -- the two levels overlap, so the split is of launches, not of levels.
   const size_t per = (D + c->dual_chunks - 1) / c->dual_chunks;
-  if (c->dual && c->trace_fft && !split && !guarded(c, 0) && !guarded(c, 1) && D >= 2 && !latency_path(c, std::min(per, c->batch))) {
+  if (c->dual && c->trace_fft && !split && !c->exact1 && !guarded(c, 0) && !guarded(c, 1) && D >= 2 && !latency_path(c, std::min(per, c->batch))) {
     const size_t B = std::min(per, c->batch), nch = (D + B - 1) / B;
     if (c->timing) {
       while (c->events.size() < nch * EV_PER_CHUNK) {
@@ -1550,7 +1569,7 @@ extern "C" omr_status omr_first_level(omr_ctx *c, const uint16_t *ca, const uint
   HIP_TRY(hipMemcpyAsync(lwe_int, c->lwe_int, D * (NI + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   if ((s = scratch_release(c, st)) != OMR_OK) return s;
   HIP_TRY(hipStreamSynchronize(st));
-  return take_handoff_error(c);  // an uncertified level-1 product (the exactness contract)
+  return OMR_OK;
 }
 
 extern "C" omr_status omr_fft1_mul(omr_ctx *c, const uint32_t *a, const uint32_t *k, size_t n,

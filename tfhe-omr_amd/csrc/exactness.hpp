@@ -142,18 +142,15 @@ struct RoundGuard {
 // Guard words per context: [0, 1] the largest margin of levels 1, 2 since the last reset (what
 // omr_ctx_rounding_margin reports), [2, 3] the margin of the launch in flight (zeroed before each
 // guarded launch, written by its kernels), [4, 5] the number of launches whose margin reached the
-// threshold 1 - E (level 1: reported as OMR_ERR_INEXACT through bit GUARD_ERR_INEXACT of the
-// context's error word; level 2: that launch was re-run on the exact NTT, br2l_fallback_kernel).
+// threshold 1 - E (that launch was then re-run on the exact NTT: br1n_fallback_kernel,
+// br2l_fallback_kernel + trace_fallback_kernel).
 constexpr int GUARD_WORDS = 6;
-constexpr int GUARD_ERR_HANDOFF = 1, GUARD_ERR_INEXACT = 2;
-__global__ void guard_fold_kernel(unsigned long long *words, int level, double thr, int *err) {
+constexpr int GUARD_ERR_HANDOFF = 1;  // bit of the context's error word: a two-CU hand-off timed out
+__global__ void guard_fold_kernel(unsigned long long *words, int level, double thr) {
   if (threadIdx.x != 0) return;
   const unsigned long long m = words[2 + level];
   atomicMax(&words[level], m);
-  if (__longlong_as_double((long long)m) >= thr) {
-    atomicAdd(&words[4 + level], 1ull);
-    if (level == 0) atomicOr(err, GUARD_ERR_INEXACT);
-  }
+  if (__longlong_as_double((long long)m) >= thr) atomicAdd(&words[4 + level], 1ull);
 }
 
 }  // namespace omr

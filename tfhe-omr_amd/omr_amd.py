@@ -73,6 +73,7 @@ EXPORTS = {
     "omr_ctx_destroy": (None, [C.c_void_p]),
     "omr_ctx_set_batch": (C.c_int, [C.c_void_p, C.c_size_t]),
     "omr_ctx_set_latency_threshold": (C.c_int, [C.c_void_p, C.c_size_t]),
+    "omr_ctx_set_exact_level1": (C.c_int, [C.c_void_p, C.c_int]),
     "omr_ctx_set_encode_chunks": (C.c_int, [C.c_void_p, C.c_size_t]),
     "omr_detect_batch": (C.c_int, [C.c_void_p, _u16p, _u16p, C.c_size_t, _u64p]),
     "omr_detect": (C.c_int, [C.c_void_p, _u16p, _u16p, _u64p]),
@@ -441,6 +442,11 @@ class Detector:
         """Chunks of at most max_messages messages use the latency kernels (0: never)."""
         _check(lib().omr_ctx_set_latency_threshold(self._h, max_messages), "omr_ctx_set_latency_threshold")
 
+    def set_exact_level1(self, enable: bool = True):
+        """Level 1 on the exact modular NTT for every launch (omr_ctx_set_exact_level1: the
+        reference's arithmetic, bit-identical outputs, slower); False restores the FFT kernels."""
+        _check(lib().omr_ctx_set_exact_level1(self._h, 1 if enable else 0), "omr_ctx_set_exact_level1")
+
     # detect (detector.rs:135) — one clue set -> NttRlweCiphertext [2][2048]
     def detect(self, clue_a, clue_b) -> np.ndarray:
         """One message (omr_detect): thread-safe; concurrent callers are coalesced into batched
@@ -493,7 +499,7 @@ class Detector:
     def exactness(self) -> dict:
         """The exactness contract (omr_ctx_exactness): {"guarded": [l1, l2] guarded on every launch
         (automatically when the key's a priori bound E >= 0.5), "breaches": [l1, l2] launches whose
-        margin reached 1 - E (level 2: re-run on the exact NTT; level 1: OMR_ERR_INEXACT)}."""
+        margin reached 1 - E (each such launch re-run on the exact NTT)}."""
         g, b = (C.c_int * 2)(), (C.c_uint64 * 2)()
         _check(lib().omr_ctx_exactness(self._h, g, b), "omr_ctx_exactness")
         return {"guarded": [bool(v) for v in g], "breaches": list(b)}
