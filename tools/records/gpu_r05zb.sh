@@ -1,0 +1,9 @@
+#!/bin/bash
+# Round 5, call ZB: the full GPU suite, smoke and the default bench line at the HEAD with level 1's
+# exact NTT (the breach fallback and omr_ctx_set_exact_level1).
+export TMPDIR=/tmp
+mkdir -p gpurun_out/r05zb
+tools/gpu_step.sh 900 r05zb/gpu_tests.log python -u -m pytest tests -m gpu -v -rP --timeout 600 --timeout-method thread || exit 99
+grep -q "passed" gpurun_out/r05zb/gpu_tests.log && ! grep -q "FAILED" gpurun_out/r05zb/gpu_tests.log || { echo "suite failed"; exit 98; }
+tools/gpu_step.sh 300 r05zb/smoke.log python -c "import __graft_entry__ as g; g.smoke()" || exit 99
+tools/gpu_step.sh 600 r05zb/bench.json python bench.py || exit 99
