@@ -570,12 +570,14 @@ __device__ __forceinline__ void br2f_body(const uint32_t *__restrict__ lwe_int, 
   const __amdgpu_buffer_rsrc_t rsrc = bsk2_rsrc(bskf);
   const uint32_t t16 = (uint32_t)t * 16u;
   RoundGuard<G> rg;
+  int kq = -1;  // the row whose output-A blocks ka already holds (the previous step's last digit loads them)
 #pragma unroll 1
   for (int i = 0; i < NI; ++i) {
     const int a = (int)__builtin_amdgcn_readfirstlane(lwe[i]) & (2 * NN - 1);
     if (a == 0) continue;  // (X^0 - 1) * ACC = 0
     const int q0 = i * 2 * D2;  // the step's first global row
-    br2f_load_half(ka, rsrc, q0, 0, t16);
+    if (kq != q0) br2f_load_half(ka, rsrc, q0, 0, t16);
+    kq = i + 1 < NI ? q0 + 2 * D2 : -1;
     wg_barrier_lds();  // ACC (init or the previous update) visible; the previous inverses' reads done
     double sr[2][2][E], si[2][2][E];  // [output][limb] spectra
 #pragma unroll
@@ -583,11 +585,13 @@ __device__ __forceinline__ void br2f_body(const uint32_t *__restrict__ lwe_int, 
       uint32_t pk[2][E][Digits2S::DW];  // [coefficient j / j + 1024][point] digit words
       br2f_digits(acs + p * NN, a, t, pk);
       // digits in issue order g = 2 j + w: digit j + 3 w sits in word w at field j, so the word is
-      // chosen at compile time; its GGSW row is p D2 + j + 3 w. The next digit in issue order (the
-      // last digit reloads its own row: harmless): after (j, 0) comes (j, 1), after (j, 1)
-      // (j + 1, 0), after the mask's last digit the body's first, after the body's last itself.
+      // chosen at compile time; its GGSW row is p D2 + j + 3 w. The next digit in issue order: after
+      // (j, 0) comes (j, 1), after (j, 1) (j + 1, 0), after the mask's last digit the body's first,
+      // after the body's last the next step's first row (in flight across the inverses; kq above;
+      // the last step reloads its own row: harmless).
       auto nxt = [&](int j, int w) {
-        return q0 + (w == 0 ? p * D2 + j + 3 : (j + 1 < D2 / 2 ? p * D2 + j + 1 : (p == 0 ? D2 : 2 * D2 - 1)));
+        return q0 + (w == 0 ? p * D2 + j + 3
+                            : (j + 1 < D2 / 2 ? p * D2 + j + 1 : (p == 0 ? D2 : (kq >= 0 ? 2 * D2 : 2 * D2 - 1))));
       };
       if (p == 0) {  // (peeling the step's first digit instead measured 10 % slower: 22 spills)
 #pragma unroll
@@ -604,6 +608,8 @@ __device__ __forceinline__ void br2f_body(const uint32_t *__restrict__ lwe_int, 
       }
     }
     // inverses on X0, X1, X0, X1, rounding to the exact limb products, recombination mod q2
+    // (pipelining them in barrier stages, the second half of one beside the first half of the next,
+    // measured no faster: profiles/r05zd/bench_variants.log, var_kpi)
 #pragma unroll
     for (int o = 0; o < 2; ++o) {
 #pragma unroll
