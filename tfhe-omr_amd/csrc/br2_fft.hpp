@@ -211,12 +211,18 @@ struct Fft1024 {
   // tests/test_fft2_layout.py::test_exchange_regions), which after this transform's cross-wave reads
   // no other wave touches until the next-but-one transform writes X behind the next barrier. Every
   // pass in tangent form on the thread's (A, B) held in registers (wc[P - 1]: block_ct<P>).
+  struct NoMid {
+    __device__ void operator()() const {}
+  };
+  // mid(): called after the cross-wave exchange (br2f_digit issues key loads there)
+  template <typename Mid = NoMid>
   __device__ static __forceinline__ void fwd(double (&xr)[E], double (&xi)[E], double2 *X, int t,
-                                             const double2 (&wc)[4][2]) {
+                                             const double2 (&wc)[4][2], Mid mid = Mid()) {
     fwd_pass_t(xr, xi, make_double2(R2, 1.0), make_double2(C8, T8));
     perm(xr, xi);
     fwd_pass_t(xr, xi, wc[0][0], wc[0][1]);
     exchange<1, 2, 0, true>(xr, xi, X, t);
+    mid();
     fwd_pass_t(xr, xi, wc[1][0], wc[1][1]);
     perm(xr, xi);
     fwd_pass_t(xr, xi, wc[2][0], wc[2][1]);
@@ -343,9 +349,9 @@ __device__ __forceinline__ void br2f_digits(const double *acp, int a, int t,
 
 // One digit of a CMUX step: forward transform of digit j + 3 w (W) of the poly whose words are pk,
 // then the multiply-accumulate into the four (output, limb) spectra: output A with ka (loaded one
-// digit ahead, in flight across the transform), output B with kb (loaded after the transform, in
-// flight across output A's multiply-accumulate); ka is reloaded for the next digit nx between the
-// two. (A function, not a lambda: by-reference captures drop __restrict__ / address-space facts.)
+// digit ahead, in flight across the transform), output B with kb (limb 0 loaded mid-transform, limb 1
+// after it, in flight across output A's multiply-accumulate); ka is reloaded for the next digit nx
+// between the two. (A function, not a lambda: by-reference captures drop __restrict__ / address-space facts.)
 template <int W>
 __device__ __forceinline__ void br2f_digit(const uint32_t (&pk)[2][Fft1024::E][Digits2S::DW], int j, int q, int nx,
                                            double (&sr)[2][2][Fft1024::E], double (&si)[2][2][Fft1024::E],
@@ -359,8 +365,24 @@ __device__ __forceinline__ void br2f_digit(const uint32_t (&pk)[2][Fft1024::E][D
     xr[e] = Digits2S::digit<W>(pk[0][e], j);
     xi[e] = Digits2S::digit<W>(pk[1][e], j);
   }
-  F::fwd(xr, xi, X, t, wc);
-  br2f_load_half(kb, rsrc, q, 1, t16);
+  // output B's limb-0 blocks issued mid-transform (after its cross-wave exchange: 1.3 % faster at
+  // level 2 than after the transform; both limbs there spill and run 20-34 % slower,
+  // profiles/r05zf/bench_variants.log), limb 1 after it, in flight across output A's products
+  auto load_kb = [&](int l) {
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const uint32_t soff = (uint32_t)q * (uint32_t)(BR2_ROW * sizeof(double2)) +
+                            (uint32_t)(((1 * 2 + l) * Fft1024::n + e * Fft1024::T) * sizeof(double2));
+      kb[l][e] = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rsrc, t16, (int)soff, 0));
+    }
+  };
+  constexpr int LE = 1;  // limbs issued mid-transform (this form is the measured schedule)
+  F::fwd(xr, xi, X, t, wc, [&]() {
+#pragma unroll
+    for (int l = 0; l < LE; ++l) load_kb(l);
+  });
+#pragma unroll
+  for (int l = LE; l < 2; ++l) load_kb(l);
 #pragma unroll
   for (int o = 0; o < 2; ++o) {
 #pragma unroll
