@@ -487,8 +487,17 @@ __device__ __forceinline__ void br2f_trace(double *acs, const double2 *__restric
         xr[e] = DigitsTrace::get(pk[0][e], d);
         xi[e] = DigitsTrace::get(pk[1][e], d);
       }
-      F::fwd(xr, xi, Xb[d & 1], t, wc);
-      br2f_load_half(kb, rsrc, q, 1, t16);
+      // output B's limb-0 blocks mid-transform, limb 1 after it (as br2f_digit)
+      auto load_kb = [&](int l) {
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const uint32_t soff = (uint32_t)q * (uint32_t)(BR2_ROW * sizeof(double2)) +
+                                (uint32_t)(((1 * 2 + l) * Fft1024::n + e * Fft1024::T) * sizeof(double2));
+          kb[l][e] = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rsrc, t16, (int)soff, 0));
+        }
+      };
+      F::fwd(xr, xi, Xb[d & 1], t, wc, [&]() { load_kb(0); });
+      load_kb(1);
 #pragma unroll
       for (int o = 0; o < 2; ++o) {
 #pragma unroll
@@ -631,7 +640,8 @@ __device__ __forceinline__ void br2f_body(const uint32_t *__restrict__ lwe_int, 
     }
     // inverses on X0, X1, X0, X1, rounding to the exact limb products, recombination mod q2
     // (pipelining them in barrier stages, the second half of one beside the first half of the next,
-    // measured no faster: profiles/r05zd/bench_variants.log, var_kpi)
+    // measured no faster: profiles/r05zd/bench_variants.log, var_kpi; nor reading the accumulator
+    // entries ahead of each output's last inverse: profiles/r05zg/, var_upf)
 #pragma unroll
     for (int o = 0; o < 2; ++o) {
 #pragma unroll
