@@ -473,6 +473,13 @@ def main():
     role = max(kms, key=kms.get)
     chunks = -(-D // args.batch)
     roof, hbm = rooflines(role, names[role], args.steps * chunks, D / chunks, kms[role], value, world, names)
+    # the other blind rotation's roofline the same way (its own live launch time and counted FLOPs)
+    other_roofs = {}
+    for r in ("br1", "br2"):
+        if r != role:
+            ro, _ = rooflines(r, names[r], args.steps * chunks, D / chunks, kms[r], value, world, names)
+            if ro is not None:
+                other_roofs[r] = ro
     line = {
         "metric": "detect-phase messages/sec + per-message latency, D=65536 at 1/2/4/8 MI355X",
         "value": round(value, 2),
@@ -500,6 +507,7 @@ def main():
         "detect_time_info": time_info,
         "detect_bytes_per_message": DETECT_BYTES,
         "roofline": roof,
+        "roofline_other_rotation": other_roofs or None,
         "hbm": hbm,
         "correct": ok,
         "exactness": exactness,
