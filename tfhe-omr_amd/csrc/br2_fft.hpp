@@ -376,15 +376,10 @@ __device__ __forceinline__ void br2f_digit(const uint32_t (&pk)[2][Fft1024::E][D
       kb[l][e] = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rsrc, t16, (int)soff, 0));
     }
   };
-  // Wave priority (s_setprio): normal up to the transform's cross-wave barrier, raised after it
-  // through the rest of the transform and the multiply-accumulates. Of the two workgroups that
-  // share each SIMD, the wave past a barrier then issues first, so a workgroup's four waves reach
-  // the next barrier closer together: level 2 -3.4 % (profiles/r05zl/bench_variants.log, var_prio2f;
-  // the same in br1f's rows is slower there).
+  // (Raising the wave priority after the transform's cross-wave barrier made level 2 3-4 % faster
+  // in most runs but bimodal: one run in four 50 % slower, profiles/r05zn/ -- not kept.)
   constexpr int LE = 1;  // limbs issued mid-transform (this form is the measured schedule)
-  __builtin_amdgcn_s_setprio(0);
   F::fwd(xr, xi, X, t, wc, [&]() {
-    __builtin_amdgcn_s_setprio(2);
 #pragma unroll
     for (int l = 0; l < LE; ++l) load_kb(l);
   });
