@@ -376,10 +376,15 @@ __device__ __forceinline__ void br2f_digit(const uint32_t (&pk)[2][Fft1024::E][D
       kb[l][e] = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rsrc, t16, (int)soff, 0));
     }
   };
-  // (Raising the wave priority after the transform's cross-wave barrier made level 2 3-4 % faster
-  // in most runs but bimodal: one run in four 50 % slower, profiles/r05zn/ -- not kept.)
+  // Wave priority (s_setprio) raised from the transform's cross-wave barrier to the end of the
+  // digit's multiply-accumulates, normal otherwise: of the two workgroups sharing each SIMD, the wave
+  // past a barrier issues first, so a workgroup's four waves reach the next barrier closer together
+  // (level 2 -3.7 %, stable over 8 alternating runs: profiles/r05zo/). Left raised past the digit
+  // (through the inverses and the next digit words) it was as fast in most runs but bimodal, one run
+  // in four 50 % slower at level 2 (profiles/r05zn/).
   constexpr int LE = 1;  // limbs issued mid-transform (this form is the measured schedule)
   F::fwd(xr, xi, X, t, wc, [&]() {
+    __builtin_amdgcn_s_setprio(2);
 #pragma unroll
     for (int l = 0; l < LE; ++l) load_kb(l);
   });
@@ -397,6 +402,7 @@ __device__ __forceinline__ void br2f_digit(const uint32_t (&pk)[2][Fft1024::E][D
       }
     if (o == 0) br2f_load_half(ka, rsrc, nx, 0, t16);
   }
+  __builtin_amdgcn_s_setprio(0);
 }
 
 // Rounding to the exact limb products, recombination mod q2 and ACC_o += (in place in LDS): thread

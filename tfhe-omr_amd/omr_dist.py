@@ -64,10 +64,13 @@ def host_rendezvous(envs, addr: str = "127.0.0.1"):
     return store
 
 
-def spawn_ranks(argv, envs, poll_s: float = 0.5) -> int:
+def spawn_ranks(argv, envs, poll_s: float = 0.02) -> int:
     """Start one child per environment running `argv` (stdout/stderr inherited: only rank 0
     prints the result line) and wait for all of them. If any child fails, the others are
-    terminated and its exit code is returned; 0 when all succeed."""
+    terminated and its exit code is returned; 0 when all succeed. The poll interval is short so
+    that the first child to fail is the one reported: a peer whose collective then breaks exits
+    (with its own code) a few hundred ms later, and with a 0.5 s interval both could land in one
+    sweep, reported in rank order (profiles/r05zp/gpu_tests.log)."""
     import subprocess
     procs = [subprocess.Popen(argv, env=e) for e in envs]
     rc = 0
