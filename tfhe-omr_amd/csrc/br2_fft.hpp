@@ -240,9 +240,11 @@ struct Fft1024 {
     perm(xr, xi);
     inv_pass<2>(xr, xi, tws, t);
     exchange<2, 1, 1, true>(xr, xi, X, t);
+    __builtin_amdgcn_s_setprio(2);  // raised past the cross-wave barrier, as in br2f_digit
     inv_pass<1>(xr, xi, tws, t);
     perm(xr, xi);
     inv_pass<0>(xr, xi, tws, t);
+    __builtin_amdgcn_s_setprio(0);
   }
 };
 
@@ -379,7 +381,8 @@ __device__ __forceinline__ void br2f_digit(const uint32_t (&pk)[2][Fft1024::E][D
   // Wave priority (s_setprio) raised from the transform's cross-wave barrier to the end of the
   // digit's multiply-accumulates, normal otherwise: of the two workgroups sharing each SIMD, the wave
   // past a barrier issues first, so a workgroup's four waves reach the next barrier closer together
-  // (level 2 -3.7 %, stable over 8 alternating runs: profiles/r05zo/). Left raised past the digit
+  // (level 2 -3.7 %, stable over 8 alternating runs: profiles/r05zo/; the inverses the same way,
+  // Fft1024::inv: profiles/r05zq/). Left raised past the digit
   // (through the inverses and the next digit words) it was as fast in most runs but bimodal, one run
   // in four 50 % slower at level 2 (profiles/r05zn/).
   constexpr int LE = 1;  // limbs issued mid-transform (this form is the measured schedule)
