@@ -54,11 +54,7 @@ typedef enum {
   OMR_ERR_INVALID_ARGUMENT = 1,
   OMR_ERR_DEVICE = 2,
   OMR_ERR_OUT_OF_MEMORY = 3,
-  OMR_ERR_NOT_INVERTIBLE = 4, /* OmrError::InvertibleMatrix, error.rs:5-8 */
-  /* Reserved (kept for ABI stability): up to round 5 an uncertified level-1 FFT product was reported
-   * with this code; such a launch is now re-run on the exact NTT (omr_ctx_exactness), so no call
-   * returns it. */
-  OMR_ERR_INEXACT = 5
+  OMR_ERR_NOT_INVERTIBLE = 4 /* OmrError::InvertibleMatrix, error.rs:5-8 */
 } omr_status;
 
 /* Message of the last failing call on this thread ("" if none). */
@@ -200,8 +196,7 @@ omr_status omr_ctx_rounding_margin(omr_ctx *ctx, double observed[2], double apri
  *  - level 2: a launch with m >= 1 - E2 is re-run on the exact modular NTT (the latency family's
  *    br2l_kernel + trace), in the same stream order, so its outputs are exact;
  *  - level 1: a launch with m >= 1 - E1 is re-run on the exact modular NTT (br1n_fallback_kernel,
- *    br1_ntt.hpp) in the same stream order, so its outputs are exact (round 5; before, such a launch
- *    was reported as OMR_ERR_INEXACT, a code no call returns any more).
+ *    br1_ntt.hpp) in the same stream order, so its outputs are exact.
  * guarded[l] != 0 when level l + 1 is guarded on every launch (automatically or by the user);
  * breaches[l] counts the launches of level l + 1 whose margin reached the threshold. Any pointer
  * may be NULL. Reading breaches synchronises the device. */

@@ -32,8 +32,6 @@ pub mod ffi {
     pub const OMR_ERR_DEVICE: OmrStatus = 2;
     pub const OMR_ERR_OUT_OF_MEMORY: OmrStatus = 3;
     pub const OMR_ERR_NOT_INVERTIBLE: OmrStatus = 4;
-    /// reserved: no call returns it since level-1 breaches are re-run on the exact NTT
-    pub const OMR_ERR_INEXACT: OmrStatus = 5;
 
     pub const OMR_N0: usize = 512;
     pub const OMR_Q0: u32 = 2048;
@@ -496,8 +494,9 @@ impl GpuDetector {
     }
 
     /// The exactness contract (`omr_ctx_exactness`): (guarded on every launch, breaching launches)
-    /// per level. A level whose a priori bound is >= 0.5 is guarded automatically; a level-2 breach
-    /// (either level) was re-run on the exact NTT.
+    /// per level. A level whose a priori bound is >= 0.5 is guarded automatically; a breach on
+    /// either level was re-run on the exact NTT (level 1: br1n_fallback_kernel; level 2:
+    /// br2l_fallback_kernel + trace_fallback_kernel).
     pub fn exactness(&self) -> Result<([bool; 2], [u64; 2]), OmrError> {
         let (mut g, mut b) = ([0 as c_int; 2], [0u64; 2]);
         check(unsafe { omr_ctx_exactness(self.ctx, g.as_mut_ptr(), b.as_mut_ptr()) })?;

@@ -157,36 +157,3 @@ def test_encode_rejects_bad_shapes(ctx):
     rp = A.RetrievalParams(3, 1)  # board smaller than offset + D
     with pytest.raises(A.OmrError):
         det.encode_pertinent_indices(rp, pv, 9, 0)
-
-
-@pytest.mark.parametrize("D,chunks", [(20000, 8), (65536, 4)])
-def test_dual_pipeline_matches_sequential(ctx, monkeypatch, D, chunks):
-    """The co-scheduled pipeline (OMR_DUAL=1: level 1 of chunk k + 1 and level 2 of chunk k in one
-    dual_kernel launch, dual_kernel.hpp) against the sequential launches of the module's detector,
-    every output bit for bit, at a ragged chunking (20,000 = 8 chunks of 2,500) and at bench.py's
-    D = 65,536 in 4 chunks; plus the KAT on every output."""
-    import torch
-    a, b, det, _ = ctx
-    rng = np.random.default_rng(77 + D)
-    mask = np.zeros(D, dtype=bool)
-    mask[np.sort(rng.choice(D, 40, replace=False))] = True
-    d_ca, d_cb = _device_clues(a, b, D, 5000, mask)
-    monkeypatch.setenv("OMR_DUAL", "1")
-    monkeypatch.setenv("OMR_DUAL_CHUNKS", str(chunks))
-    _, _, dk = PL.keys()
-    dual = A.Detector(dk)
-    monkeypatch.delenv("OMR_DUAL")
-    monkeypatch.delenv("OMR_DUAL_CHUNKS")
-    try:
-        outs = []
-        for d in (dual, det):
-            o = torch.empty((D, 2, 2048), dtype=torch.int64, device="cuda:0")
-            d.set_batch(D)
-            d.detect_batch_device(d_ca.data_ptr(), d_cb.data_ptr(), D, o.data_ptr(), 0)
-            d.set_batch(0)
-            torch.cuda.synchronize()
-            outs.append(o)
-        assert torch.equal(outs[0], outs[1])
-        _kat_all(a, outs[0], mask)
-    finally:
-        dual.close()

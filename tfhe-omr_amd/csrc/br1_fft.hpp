@@ -270,7 +270,7 @@ __device__ __forceinline__ void br1f_step_lds(uint32_t (&ac)[2][16], double2 *xc
 // g. The transforms are wave-private (wave-level LDS sync); the waves run the CMUX steps in
 // lockstep, sharing each key row staged in LDS and one twiddle table.
 // G: the rounding-margin guard (exactness.hpp) publishes the largest |y - rint(y)| to *margin.
-// LDS of br1f_body, carved from a pool (so that dual_kernel can overlay it with br2f_body's):
+// LDS of br1f_body, carved from one pool:
 // the exchange buffers (8 KB-aligned: br1f_digits' addressing), the twiddles, the LWE masks, the two
 // staged key rows: 76 KB.
 constexpr size_t BR1_LDS_XCH = 0, BR1_LDS_TWS = BR1_LDS_XCH + (size_t)BR1F_WPG * Fft512::BUF * sizeof(double2),

@@ -570,7 +570,7 @@ __device__ __forceinline__ void br2f_trace(double *acs, const double2 *__restric
 // use rewrites a buffer whose readers have passed a later barrier: 17 workgroup barriers per step
 // (one at the step start: the previous update visible to the rotated reads).
 // LDS: twiddles 16 KB, X0 / X1 32 KB, ACC 32 KB (80 KB: two workgroups per CU).
-// LDS of br2f_body, carved from a pool (dual_kernel overlays it with br1f_body's): the twiddles,
+// LDS of br2f_body, carved from one pool: the twiddles,
 // then X0, X1, ACC (mask, body); the trace's 3 N2 doubles afterwards: 80 KB.
 constexpr size_t BR2_LDS_X = 0, BR2_LDS_TWS = 4 * (size_t)Fft1024::n * sizeof(double2),
                  BR2_LDS_BYTES = BR2_LDS_TWS + (size_t)Fft1024::n * sizeof(double2);

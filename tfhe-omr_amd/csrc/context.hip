@@ -19,7 +19,6 @@
 #include "br1_ntt.hpp"
 #include "br2_fft.hpp"
 #include "detect_kernels.hpp"
-#include "dual_kernel.hpp"
 #include "encode_kernels.hpp"
 #include "key_spectra.hpp"
 #include "latency_kernels.hpp"
@@ -285,6 +284,9 @@ struct omr_ctx {
   double2 *bsk1f = nullptr;  // level-1 FFT-domain keys [512][8][2][512] complex, x 1/512
   double2 *bsk1l = nullptr;  // the same in br1l_kernel's layout [512][8 slot][8 row][2][64 lane]
   double *bsk1n = nullptr;   // BSK1 in the NTT domain x 1/1024 [512][8][2][1024] (br1_ntt.hpp: level 1's exact path)
+  // the coefficient-domain BSK1 kept on the host (32 MB) until bsk1n is built: bsk1n (64 MB of HBM)
+  // is converted lazily, only when level 1 is guarded or run exactly (ensure_bsk1n)
+  std::vector<uint32_t> bsk1_host;
   double2 *fft1 = nullptr;   // level-1 FFT twiddles
   double *bsk2 = nullptr, *tk = nullptr;  // BSK2 NTT domain (latency kernels), trace key
   double2 *bsk2f = nullptr;                // BSK2 as FFT-domain 25-bit limbs (br2f_kernel), x 1/1024
@@ -336,11 +338,6 @@ struct omr_ctx {
   bool br2y = true;
   bool no_prefetch = false;  // OMR_PREFETCH=0: the latency kernels launch no key-prefetch helpers
   bool no_fast_handoff = false;  // OMR_FAST_HANDOFF=0: br2y keeps the sc1 hand-off on one XCD too
-  // co-scheduled levels (dual_kernel.hpp): OMR_DUAL=1 at context creation; a detect call of D
-  // messages is cut into dual_chunks chunks so that level 1 of chunk k + 1 runs beside level 2 of k
-  bool dual = false;
-  int dual_chunks = 8;
-  unsigned *dual_ctl = nullptr;
   // host-API staging
   uint16_t *s_clue_a = nullptr, *s_clue_b = nullptr;
   uint64_t *s_out = nullptr;
@@ -554,6 +551,24 @@ omr_status guard_begin(omr_ctx *c, int level, hipStream_t st) {
 omr_status guard_end(omr_ctx *c, int level, hipStream_t st) {
   guard_fold_kernel<<<1, 64, 0, st>>>(c->margin, level, c->thr[level]);
   HIP_TRY(hipGetLastError());
+  return OMR_OK;
+}
+
+// Level 1's exact-NTT key (br1n_kernel / br1n_fallback_kernel), built on first need: when level 1
+// is guarded (the exactness contract's re-run target) or run exactly. Callers hold c->mu (or own c).
+omr_status ensure_bsk1n(omr_ctx *c) {
+  if (c->bsk1n) return OMR_OK;
+  if (c->bsk1_host.size() != BSK1_ELEMS)
+    return set_error(OMR_ERR_DEVICE, "ensure_bsk1n: the coefficient-domain BSK1 is gone");
+  HIP_TRY(hipMalloc(&c->bsk1n, BSK1_ELEMS * sizeof(double)));
+  const double ninv1 = centred(h_powmod(N1, Q1 - 2, Q1), Q1);
+  omr_status s;
+  if ((s = convert_keys<1, uint32_t, double>(c->bsk1_host.data(), BSK1_ELEMS / N1, c->bsk1n, ninv1, c->tb.tw1,
+                                             c->stream)) != OMR_OK) {
+    dev_free(c->bsk1n);
+    return s;
+  }
+  std::vector<uint32_t>().swap(c->bsk1_host);
   return OMR_OK;
 }
 
@@ -788,10 +803,6 @@ extern "C" omr_status omr_ctx_create(const omr_detection_key_view *key, int devi
     c->no_prefetch = ep && ep[0] == '0';
     const char *eh = getenv("OMR_FAST_HANDOFF");
     c->no_fast_handoff = eh && eh[0] == '0';
-    const char *ed = getenv("OMR_DUAL");
-    c->dual = ed && ed[0] == '1';
-    const char *ec = getenv("OMR_DUAL_CHUNKS");
-    if (ec && atoi(ec) >= 2) c->dual_chunks = atoi(ec);
   }
   auto fail = [&](omr_status st) {
     omr_ctx_destroy(c);
@@ -866,7 +877,6 @@ extern "C" omr_status omr_ctx_create(const omr_detection_key_view *key, int devi
   // keys
   if (hipMalloc(&c->bsk1f, BSK1_ELEMS / 2 * sizeof(double2)) != hipSuccess ||
       hipMalloc(&c->bsk1l, BSK1_ELEMS / 2 * sizeof(double2)) != hipSuccess ||
-      hipMalloc(&c->bsk1n, BSK1_ELEMS * sizeof(double)) != hipSuccess ||
       hipMalloc(&c->bsk2, BSK2_ELEMS * sizeof(double)) != hipSuccess ||
       hipMalloc(&c->bsk2f, BSK2_ELEMS * sizeof(double2)) != hipSuccess ||
       hipMalloc(&c->tk, TK_ELEMS * sizeof(double)) != hipSuccess ||
@@ -879,10 +889,9 @@ extern "C" omr_status omr_ctx_create(const omr_detection_key_view *key, int devi
   bsk1_latency_layout_kernel<<<(unsigned)(BSK1_ELEMS / 2 / 256), 256, 0, c->stream>>>(c->bsk1f, c->bsk1l,
                                                                                      BSK1_ELEMS / 2);
   if (hipGetLastError() != hipSuccess) return fail(set_error(OMR_ERR_DEVICE, "omr_ctx_create: BSK1 layout"));
-  const double ninv1 = centred(h_powmod(N1, Q1 - 2, Q1), Q1);
-  if ((st = convert_keys<1, uint32_t, double>(key->bsk1, BSK1_ELEMS / N1, c->bsk1n, ninv1, c->tb.tw1,
-                                              c->stream)) != OMR_OK)
-    return fail(st);
+  c->bsk1_host.resize(BSK1_ELEMS);  // for ensure_bsk1n (the view may point to host or device memory)
+  if (hipMemcpy(c->bsk1_host.data(), key->bsk1, BSK1_ELEMS * sizeof(uint32_t), hipMemcpyDefault) != hipSuccess)
+    return fail(set_error(OMR_ERR_DEVICE, "omr_ctx_create: BSK1 copy"));
   if ((st = convert_keys_cmux(key->bsk2, BSK2_ELEMS / N2, c->bsk2, ninv2, c->tb.tw2c, c->stream)) != OMR_OK)
     return fail(st);
   if ((st = convert_keys_dd<2>(key->bsk2, BSK2_ELEMS / N2, c->bsk2f, c->stream)) != OMR_OK) return fail(st);
@@ -921,6 +930,7 @@ extern "C" omr_status omr_ctx_create(const omr_detection_key_view *key, int devi
     // the fused FFT trace shares level 2's guard word and threshold
     if (c->trace_fft) c->thr[1] = 1.0 - std::max(c->apriori[1], c->apriori_t);
   }
+  if (c->guard_auto[0] && (st = ensure_bsk1n(c)) != OMR_OK) return fail(st);
   if ((st = convert_keys<2, uint64_t, double>(key->trace_key, TK_ELEMS / N2, c->tk, 1.0, c->tb.tw2,
                                               c->stream)) != OMR_OK)
     return fail(st);
@@ -967,7 +977,6 @@ extern "C" void omr_ctx_destroy(omr_ctx *c) {
   dev_free(c->ks_part);
   dev_free(c->x_slots);
   dev_free(c->x_flags);
-  dev_free(c->dual_ctl);
   dev_free(c->t_slots);
   dev_free(c->t_flags);
   dev_free(c->margin);
@@ -1016,6 +1025,9 @@ extern "C" omr_status omr_ctx_enable_timing(omr_ctx *c, int mode) {
 extern "C" omr_status omr_ctx_set_rounding_guard(omr_ctx *c, int enable) {
   if (!c) return set_error(OMR_ERR_INVALID_ARGUMENT, "omr_ctx_set_rounding_guard: NULL ctx");
   std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  omr_status s;
+  if (enable && (s = ensure_bsk1n(c)) != OMR_OK) return s;  // a guarded level-1 launch may re-run exactly
   c->guard = enable != 0;
   return OMR_OK;
 }
@@ -1023,6 +1035,9 @@ extern "C" omr_status omr_ctx_set_rounding_guard(omr_ctx *c, int enable) {
 extern "C" omr_status omr_ctx_set_exact_level1(omr_ctx *c, int enable) {
   if (!c) return set_error(OMR_ERR_INVALID_ARGUMENT, "omr_ctx_set_exact_level1: NULL ctx");
   std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  omr_status s;
+  if (enable && (s = ensure_bsk1n(c)) != OMR_OK) return s;
   c->exact1 = enable != 0;
   return OMR_OK;
 }
@@ -1098,22 +1113,6 @@ namespace {
 
 constexpr int EV_PER_CHUNK = 5;
 
-// Level 1 of B1 messages (clues ca1 / cb1 -> c->ext) beside level 2 + trace of B2 messages
-// (c->lwe_int -> out2) in one dual_kernel launch.
-omr_status launch_dual(omr_ctx *c, size_t B1, const uint16_t *ca1, const uint16_t *cb1, size_t B2, uint64_t *out2,
-                       hipStream_t st) {
-  if (!c->dual_ctl) HIP_TRY(hipMalloc(&c->dual_ctl, DUAL_CTL_WORDS * sizeof(unsigned)));
-  HIP_TRY(hipMemsetAsync(c->dual_ctl, 0, DUAL_CTL_WORDS * sizeof(unsigned), st));
-  const size_t nrot = B1 * CLUES;
-  const unsigned n1 = (unsigned)((nrot + BR1F_WPG - 1) / BR1F_WPG), n2 = (unsigned)B2;
-  dual_kernel<<<n1 + n2, 256, 0, st>>>(ca1, cb1, c->bsk1f, c->ext, nrot, n1, c->lwe_int, c->bsk2f, c->fft2, out2, n2,
-                                       c->tb, c->dual_ctl);
-  HIP_TRY(hipGetLastError());
-  trace_fft_kernel<<<n2, Fft1024::T, 0, st>>>(out2, c->tkf, c->fft2, c->tb);
-  HIP_TRY(hipGetLastError());
-  return OMR_OK;
-}
-
 // Detect D messages of device buffers on st, in chunks of c->batch: per chunk br1f (7 rotations
 // per message) -> sum7 -> key switch -> br2 + trace. Stage events per chunk: [0] br1 start,
 // [1] br1 end, [2] key switch end, [3] level-2 rotation end, [4] trace end (the trace is its own
@@ -1136,52 +1135,6 @@ omr_status detect_device(omr_ctx *c, const uint16_t *ca, const uint16_t *cb, siz
     c->timed_split = true;
   }
   if ((s = scratch_acquire(c, st)) != OMR_OK) return s;
-  // co-scheduled levels (dual_kernel.hpp): chunks of about D / dual_chunks; level 1 of the first,
-  // then per chunk k + 1 one dual launch (its level 1 beside chunk k's level 2), sum7 and key
-  // switch, and chunk k's level 2 (the last alone). Stage events: [0] / [1] around chunk k's level 1
-  // (the dual launch that carries it), [2] after its key switch, [3] = [4] after the launch that
-  // carries its level 2 -- the two levels overlap, so the split is of launches, not of levels.
-  const size_t per = (D + c->dual_chunks - 1) / c->dual_chunks;
-  if (c->dual && c->trace_fft && !split && !c->exact1 && !guarded(c, 0) && !guarded(c, 1) && D >= 2 && !latency_path(c, std::min(per, c->batch))) {
-    const size_t B = std::min(per, c->batch), nch = (D + B - 1) / B;
-    if (c->timing) {
-      while (c->events.size() < nch * EV_PER_CHUNK) {
-        hipEvent_t e;
-        HIP_TRY(hipEventCreate(&e));
-        c->events.push_back(e);
-      }
-      c->timed_chunks = nch;
-      c->timed_split = false;
-    }
-    auto ev = [&](size_t ch, int k) -> omr_status {
-      if (c->timing) HIP_TRY(hipEventRecord(c->events[ch * EV_PER_CHUNK + k], st));
-      return OMR_OK;
-    };
-    auto front = [&](size_t ch) -> omr_status {  // chunk ch: sum7 + key switch after its level 1
-      const int Bc = (int)std::min(B, D - ch * B);
-      const size_t n7 = (size_t)Bc * (N1 + 1);
-      sum7_kernel<<<(unsigned)((n7 + 255) / 256), 256, 0, st>>>(c->ext, c->lwe1t, Bc);
-      omr_status r;
-      if ((r = launch_ks(c, Bc, c->lwe_int, st)) != OMR_OK) return r;
-      return ev(ch, 2);
-    };
-    if ((s = ev(0, 0)) != OMR_OK) return s;
-    if ((s = launch_br1(c, std::min(B, D) * CLUES, ca, cb, nullptr, nullptr, c->ext, nullptr, 0, st,
-                        std::min(B, D))) != OMR_OK)
-      return s;
-    if ((s = ev(0, 1)) != OMR_OK || (s = front(0)) != OMR_OK) return s;
-    for (size_t ch = 0; ch + 1 < nch; ++ch) {
-      const size_t o1 = (ch + 1) * B, B1 = std::min(B, D - o1), o2 = ch * B;
-      if ((s = ev(ch + 1, 0)) != OMR_OK) return s;
-      if ((s = launch_dual(c, B1, ca + o1 * N0, cb + o1 * CLUES, B, out + o2 * 2 * N2, st)) != OMR_OK) return s;
-      if ((s = ev(ch + 1, 1)) != OMR_OK || (s = ev(ch, 3)) != OMR_OK || (s = ev(ch, 4)) != OMR_OK) return s;
-      if ((s = front(ch + 1)) != OMR_OK) return s;
-    }
-    const size_t ol = (nch - 1) * B;
-    if ((s = launch_br2(c, D - ol, c->lwe_int, out + ol * 2 * N2, 0, st, false, nullptr)) != OMR_OK) return s;
-    if ((s = ev(nch - 1, 3)) != OMR_OK || (s = ev(nch - 1, 4)) != OMR_OK) return s;
-    return scratch_release(c, st);
-  }
   for (size_t ch = 0; ch < nchunks; ++ch) {
     const size_t off = ch * c->batch;
     const int B = (int)std::min(c->batch, D - off);
@@ -1605,10 +1558,16 @@ extern "C" omr_status omr_blind_rotate_level1(omr_ctx *c, const uint16_t *la, co
   HIP_TRY(dout.alloc(n * 2 * N1));
   HIP_TRY(hipMemcpy(da.p, la, n * N0 * sizeof(uint16_t), hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(db.p, lb, n * sizeof(uint16_t), hipMemcpyHostToDevice));
-  omr_status s = launch_br1(c, n, nullptr, nullptr, da.p, db.p, nullptr, dout.p, 1, c->stream, n);
-  if (s != OMR_OK) return s;
-  HIP_TRY(hipStreamSynchronize(c->stream));
+  // a pending hand-off error belongs to an earlier detect call: report it before this launch (as
+  // detect_device does) instead of discarding a valid level-1 output after it
+  omr_status s;
   if ((s = take_handoff_error(c)) != OMR_OK) return s;
+  // the guarded sequence (guard_begin, guard kernel, br1n_fallback, guard_fold) uses the context's
+  // per-launch margin word, shared with every other call: serialise it with them like any scratch
+  if ((s = scratch_acquire(c, c->stream)) != OMR_OK) return s;
+  if ((s = launch_br1(c, n, nullptr, nullptr, da.p, db.p, nullptr, dout.p, 1, c->stream, n)) != OMR_OK) return s;
+  if ((s = scratch_release(c, c->stream)) != OMR_OK) return s;
+  HIP_TRY(hipStreamSynchronize(c->stream));
   HIP_TRY(hipMemcpy(out, dout.p, n * 2 * N1 * sizeof(uint64_t), hipMemcpyDeviceToHost));
   return OMR_OK;
 }
