@@ -68,6 +68,22 @@ L2_CEILING_TBPS = 30.59
 # FFT-form BSK2 (670 steps x 12 rows x 2 outputs x 2 limbs x 1024 points x 16 B; no workgroup
 # shares a row), br1f the FFT-form BSK1 rows staged by LDS-DMA once per 4-rotation workgroup.
 L2_KEY_BYTES = {"br2": 670 * 12 * 4 * 1024 * 16, "br1": 7 * 512 * 8 * 2 * 512 * 16 // 4}
+# Fixed algorithmic FP64 work per message ("fixed-work FLOPs"): a radix-2 complex
+# butterfly counts 10 FLOPs (one complex product, two complex additions), an n-point complex FFT
+# (n/2) log2 n butterflies, a complex multiply-accumulate 8 FLOPs; rounding, digit extraction and
+# recombination count nothing. Constant across rounds: an FMA or tangent-form rewrite of the same
+# transforms cannot move it (the counter-based `frac` counts FMA = 2 and can).
+#   level 1: 7 rotations x 512 steps x [10 transforms of 512 points (8 digits forward, 2 inverse)
+#            + 8 rows x 2 outputs x 512 points MAC]
+#   level 2: 670 steps x [16 transforms of 1,024 points (12 digits forward, 4 inverse: 2 outputs x
+#            2 key limbs) + 12 rows x 2 outputs x 2 limbs x 1,024 points MAC]
+#   trace:   11 automorphisms x [29 transforms of 1,024 points (25 digits, 4 inverse) + 25 rows x
+#            2 outputs x 2 limbs x 1,024 points MAC]
+FIXED_FLOP_PER_MSG = {
+    "br1": 7 * 512 * (10 * (512 // 2) * 9 * 10 + 8 * 2 * 512 * 8),         # 1,060.6 M
+    "br2": 670 * (16 * (1024 // 2) * 10 * 10 + 12 * 2 * 2 * 1024 * 8),     #   812.3 M
+    "trace": 11 * (29 * (1024 // 2) * 10 * 10 + 25 * 2 * 2 * 1024 * 8),    #    25.3 M
+}
 PUBLISHED_CPU_MS_PER_MSG = 234.073003  # README.md:122, 1 thread, AVX-512 CPU (model not stated)
 WEIGHT_SEED = bytes(range(1, 33))
 INDEX_SEED = 9
@@ -92,6 +108,9 @@ def parse():
     ap.add_argument("--one-device", action="store_true",
                     help="rehearsal of the N > 1 path on a one-GPU box: every rank uses device 0 and the "
                          "process group is gloo (RCCL cannot run two ranks on one GPU); not a scaling number")
+    ap.add_argument("--dist-timeout", type=float, default=120.0,
+                    help="seconds before a collective or the rendezvous fails (N > 1): a stuck rank ends the "
+                         "run with a non-zero exit instead of a hang")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-latency", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the encode + reduce + retrieval pass")
@@ -239,6 +258,10 @@ def rooflines(role, dom, launches, per_launch_msgs, launch_ms_total, value, worl
                 "valu_issue_frac": round(k.get("valu_lane_instr_per_msg", 0.0) * per_launch_msgs / avg_launch_s
                                          / (FP64_PEAK_TFLOPS / 2 * 1e12), 4),
                 "counts_from": comp.get("source")}
+    if roof is not None and role in FIXED_FLOP_PER_MSG:
+        fixed = FIXED_FLOP_PER_MSG[role] * per_launch_msgs / avg_launch_s / 1e12
+        roof.update({"fixed_flop_per_msg": FIXED_FLOP_PER_MSG[role], "achieved_fixed_work": round(fixed, 2),
+                     "frac_fixed_work": round(fixed / FP64_PEAK_TFLOPS, 4)})
     if roof is not None and role in L2_KEY_BYTES:
         l2 = L2_KEY_BYTES[role] * per_launch_msgs / avg_launch_s / 1e12
         roof["l2_key_stream"] = {"bytes_per_msg": L2_KEY_BYTES[role], "achieved": round(l2, 2),
@@ -283,19 +306,38 @@ def main():
     local = 0 if args.one_device else int(os.environ.get("LOCAL_RANK", "0"))
     dev = torch.device("cuda", local)
     if world > 1 or args.force_dist:
+        import datetime
         import torch.distributed as dist
         for k, v in (("MASTER_ADDR", "127.0.0.1"), ("MASTER_PORT", "29511"), ("RANK", "0"), ("WORLD_SIZE", "1")):
             os.environ.setdefault(k, v)
+        # every collective (and the rendezvous) fails after --dist-timeout seconds instead of hanging
+        # until the driver's limit: a stuck or lost rank makes bench.py exit non-zero (for RCCL the
+        # blocking wait makes work.wait() raise on the timeout instead of leaving it to the watchdog)
+        os.environ.setdefault("TORCH_NCCL_BLOCKING_WAIT", "1")
+        timeout = datetime.timedelta(seconds=args.dist_timeout)
         if args.one_device:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=timeout)
         else:
             torch.cuda.set_device(local)
-            dist.init_process_group("nccl", device_id=dev)
+            dist.init_process_group("nccl", device_id=dev, timeout=timeout)
     else:
         dist = None
     if os.environ.get("OMR_BENCH_FAIL_RANK", "") == str(rank):  # test hook: a rank that dies (tests/)
         print(f"[bench] rank {rank} failing on request (OMR_BENCH_FAIL_RANK)", file=sys.stderr, flush=True)
         sys.exit(3)
+    if os.environ.get("OMR_BENCH_HANG_RANK", "") == str(rank):  # test hook: a rank that never arrives
+        print(f"[bench] rank {rank} hanging on request (OMR_BENCH_HANG_RANK)", file=sys.stderr, flush=True)
+        time.sleep(10 * args.dist_timeout + 600)
+        sys.exit(4)
+    if dist:
+        # every rank is up and the group works, before anything expensive; the world size the
+        # process group reports goes into the result line (a SCALE record must be what it says)
+        dist.barrier()
+        world_observed = dist.get_world_size()
+        if world_observed != world:
+            raise RuntimeError(f"process group has {world_observed} ranks, WORLD_SIZE={world}")
+    else:
+        world_observed = 1
     torch.cuda.set_device(local)
     strong = args.total_messages is not None
     if strong:
@@ -341,15 +383,20 @@ def main():
         dist.barrier()
     det.enable_timing(1)  # stage events around the production kernels (trace fused into level 2)
     stage = {"first_level_ms": 0.0, "key_switch_ms": 0.0, "second_level_ms": 0.0, "trace_ms": 0.0}
+    per_step = {"first_level_ms": [], "second_level_ms": [], "step_ms": []}
     start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize(dev)
     t = time.perf_counter()
     start.record(stream)
     for i in range(args.steps):
+        ts = time.perf_counter()
         backend.detect(d_ca, d_cb, out=d_out)
         info = det.last_timing()  # per-stage HIP events recorded on `stream` (waits for them)
+        per_step["step_ms"].append((time.perf_counter() - ts) * 1e3)
         for k in stage:
             stage[k] += info[k]
+        per_step["first_level_ms"].append(info["first_level_ms"] - info["key_switch_ms"])
+        per_step["second_level_ms"].append(info["second_level_ms"])
         print(f"[bench] rank {rank} step {i + 1}/{args.steps} done", file=sys.stderr, flush=True)
     end.record(stream)
     torch.cuda.synchronize(dev)
@@ -359,10 +406,15 @@ def main():
     backend.synchronize()  # raises if a detect call failed on the device
     gpu_ms = start.elapsed_time(end)
     elapsed = max(wall, gpu_ms / 1e3)
+    rank_elapsed = [elapsed]
     if dist:
-        tt = omr_dist._on_backend(torch.tensor([elapsed], dtype=torch.float64, device=dev), dist)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+        # every rank's timed region, gathered (the line reports the spread); the value uses the max
+        tt = torch.zeros(world_observed, dtype=torch.float64, device=dev)
+        tt[rank] = elapsed
+        tt = omr_dist._on_backend(tt, dist)
+        dist.all_reduce(tt, op=dist.ReduceOp.SUM)
+        rank_elapsed = [float(v) for v in tt.tolist()]
+        elapsed = max(rank_elapsed)
 
     # Detector::detect_with_time_info's split (detector.rs:169-221) on one untimed pass: timing
     # mode 2 runs the level-2 rotation and the trace as two launches, so the trace gets its own time
@@ -390,9 +442,14 @@ def main():
     G = min(D, args.batch)
     g_out = torch.empty((G, 2, 2048), dtype=torch.int64, device=dev)
     identical = True
+    guarded_ms = 0.0
     for s0 in range(0, D, G):
         n = min(G, D - s0)
+        torch.cuda.synchronize(dev)
+        tg = time.perf_counter()
         det.detect_batch_device(d_ca[s0:].data_ptr(), d_cb[s0:].data_ptr(), n, g_out.data_ptr(), stream.cuda_stream)
+        torch.cuda.synchronize(dev)
+        guarded_ms += (time.perf_counter() - tg) * 1e3
         identical &= bool(torch.equal(g_out[:n], d_out[s0:s0 + n]))
     det.set_rounding_guard(False)
     backend.synchronize()
@@ -404,6 +461,10 @@ def main():
                  "certified": all(o < 1 - e for o, e in zip(rm["observed"], rm["apriori"])),
                  "guarded_output_identical": identical,
                  "guarded_every_launch": ex["guarded"], "breaches": ex["breaches"],
+                 # what a key with E >= 0.5 (guarded on every launch, exactness contract) would cost:
+                 # the same detect through the guarded kernels + their no-op fallbacks + the folds
+                 "guarded_ms_per_step": round(guarded_ms, 1),
+                 "guarded_over_timed": round(guarded_ms / (elapsed / args.steps * 1e3), 4),
                  "note": "level 1, level 2: largest |y - rint(y)| over every rounded FFT product coefficient "
                          "of one untimed guarded pass; exact when observed < 1 - apriori (DESIGN.md §3a); a "
                          "level with apriori >= 0.5 would be guarded on every launch (omr_ctx_exactness)"}
@@ -480,6 +541,26 @@ def main():
             ro, _ = rooflines(r, names[r], args.steps * chunks, D / chunks, kms[r], value, world, names)
             if ro is not None:
                 other_roofs[r] = ro
+    # whole-detect FP64 fractions: counted FLOPs (profiles/compute_latest.json, FMA = 2) and the fixed
+    # algorithmic FLOPs (FIXED_FLOP_PER_MSG), both at the whole job's per-GPU rate
+    comp = load_profile("compute_latest.json") or {}
+    ck = comp.get("kernels", {})
+    counted = sum(ck.get(n, {}).get("fp64_flop_per_msg", 0.0) for n in (names["br1"], names["br2"], "trace_fft_kernel"))
+    rate = value / world
+    detect_fp64 = {"counted_flop_per_msg": round(counted), "fixed_flop_per_msg": sum(FIXED_FLOP_PER_MSG.values()),
+                   "detect_fp64_frac": round(counted * rate / 1e12 / FP64_PEAK_TFLOPS, 4) if counted else None,
+                   "detect_fp64_frac_fixed_work": round(sum(FIXED_FLOP_PER_MSG.values()) * rate / 1e12
+                                                        / FP64_PEAK_TFLOPS, 4),
+                   "peak_tflops": round(FP64_PEAK_TFLOPS, 2), "counts_from": comp.get("source"),
+                   "note": "FP64 FLOPs of the whole detect (both rotations + the FFT trace) per message x the "
+                           "per-GPU msg/s over the FP64 peak; fixed_work: the constant algorithmic count of "
+                           "DESIGN.md §5 (10 FLOPs per radix-2 butterfly, 8 per complex MAC)"}
+
+    def spread(v):
+        v = sorted(v)
+        return {"min": round(v[0], 2), "median": round(float(np.median(v)), 2), "max": round(v[-1], 2),
+                "max_over_min": round(v[-1] / v[0], 4) if v[0] > 0 else None}
+
     line = {
         "metric": "detect-phase messages/sec + per-message latency, D=65536 at 1/2/4/8 MI355X",
         "value": round(value, 2),
@@ -504,6 +585,16 @@ def main():
                                   note="timed steps: first_level includes the key switch; second_level is the "
                                        "level-2 rotation (br2f_kernel), trace the FFT trace's own launch "
                                        "(trace_fft_kernel)"),
+        "per_step_spread": {"level1_rotation_ms": spread(per_step["first_level_ms"]),
+                            "level2_rotation_ms": spread(per_step["second_level_ms"]),
+                            "step_wall_ms": spread(per_step["step_ms"]),
+                            "note": "rank 0, over the K timed steps: level1 = br1f_kernel (first level minus the key "
+                                    "switch), level2 = br2f_kernel, from the stage HIP events; step_wall = host "
+                                    "wall clock of one detect call"},
+        "dist": {"world_size_observed": world_observed, "backend": dist.get_backend() if dist else None,
+                 "rank_elapsed_s": {"min": round(min(rank_elapsed), 3), "max": round(max(rank_elapsed), 3)},
+                 "timeout_s": args.dist_timeout if dist else None},
+        "detect_fp64": detect_fp64,
         "detect_time_info": time_info,
         "detect_bytes_per_message": DETECT_BYTES,
         "roofline": roof,

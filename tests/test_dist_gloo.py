@@ -201,3 +201,24 @@ def test_bench_rank_failure_propagates():
     r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--one-device",
                         "--messages", "64"], env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode != 0 and "rank 1 failing on request" in r.stderr and r.stdout == "", r.stderr[-2000:]
+
+
+def test_bench_hung_rank_times_out():
+    """bench.py --gpus 2 --one-device with rank 1 never reaching the first collective
+    (OMR_BENCH_HANG_RANK, a test hook): rank 0's barrier fails after --dist-timeout seconds, and the
+    launcher exits non-zero and kills the hung rank, well inside the limit a driver would apply
+    (a stuck rank must not hold an 8-GPU run until the driver's timeout)."""
+    import subprocess
+    import sys
+    import time
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, OMR_BENCH_HANG_RANK="1")
+    env.pop("WORLD_SIZE", None)
+    t0 = time.monotonic()
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--one-device",
+                        "--messages", "64", "--dist-timeout", "8"], env=env, capture_output=True, text=True,
+                       timeout=240)
+    took = time.monotonic() - t0
+    assert r.returncode != 0 and r.stdout == "", r.stderr[-2000:]
+    assert "rank 1 hanging on request" in r.stderr
+    assert took < 120, took

@@ -305,6 +305,15 @@ def test_bench_two_ranks_one_device_rehearsal():
     assert line["correct"] and line["exactness"]["certified"] and line["exactness"]["guarded_output_identical"]
     assert "cpu_baseline" not in line  # rank 0 of a 2-rank job reports no CPU leg
     assert all(not k.endswith("_frac") or v is None or v <= 1 for k, v in line["hbm"].items())
+    # round 6: the group's own world size, every rank's timed region, the
+    # per-step spread of both rotations, the fixed-work fractions
+    assert line["dist"]["world_size_observed"] == 2 and line["dist"]["backend"] == "gloo"
+    re_ = line["dist"]["rank_elapsed_s"]
+    assert 0 < re_["min"] <= re_["max"] and abs(line["ms_per_step"] - re_["max"] * 1e3) < 1.0
+    sp = line["per_step_spread"]
+    assert sp["level1_rotation_ms"]["min"] > 0 and sp["level2_rotation_ms"]["max_over_min"] >= 1.0
+    assert 0 < line["roofline"]["frac_fixed_work"] <= 1 and 0 < line["detect_fp64"]["detect_fp64_frac_fixed_work"] <= 1
+    assert line["exactness"]["guarded_ms_per_step"] > 0
 
 
 def test_bench_two_ranks_one_device_child_failure():
