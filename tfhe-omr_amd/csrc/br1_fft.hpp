@@ -202,7 +202,8 @@ template <bool FIRST>
 __device__ __forceinline__ void br1f_row(const uint32_t (&pk)[16], int k, int q, int qtotal, double (&outr)[2][8],
                                          double (&outi)[2][8], double2 *xch, const double2 *tws,
                                          __amdgpu_buffer_rsrc_t rsrc, double2 *kbuf, int lane, uint32_t lane16,
-                                         int wave, const double2 *__restrict__ gtw, const double2 *w3) {
+                                         int wave, const double2 *__restrict__ gtw, const double2 *w3,
+                                         const Tw1Reg &tr) {
   using F = Fft512;
   const bool more = q + 1 < qtotal;
   wg_barrier_lds();  // every wave has finished reading buffer (q + 1) & 1 (row q - 1)
@@ -213,7 +214,7 @@ __device__ __forceinline__ void br1f_row(const uint32_t (&pk)[16], int k, int q,
     xr[0][e] = Lvl1Off::digit_u(pk[e], k);
     xi[0][e] = Lvl1Off::digit_u(pk[8 + e], k);
   }
-  F::fwd<1, true>(xr, xi, xch, tws, lane, gtw, w3);
+  F::fwd<1, true, true>(xr, xi, xch, tws, lane, gtw, w3, tr);
   if (more)
     vm_wait_row_in_flight();  // row q landed (row q + 1 may stay in flight)
   else
@@ -245,19 +246,20 @@ __device__ __forceinline__ void br1f_step_lds(uint32_t (&ac)[2][16], double2 *xc
                                               __amdgpu_buffer_rsrc_t rsrc, int q0, int qtotal, double2 *kbuf,
                                               int lane, uint32_t lane16, int wave,
                                               const double2 *__restrict__ gtw, const double2 *w3,
-                                              RoundGuard<G> &rg) {
+                                              RoundGuard<G> &rg, const Tw1Reg &tr) {
   using F = Fft512;
   uint32_t pk[2][16];
   br1f_digits(ac, reinterpret_cast<uint32_t *>(xch), a, lane, pk);
   double outr[2][8], outi[2][8];
-  br1f_row<true>(pk[0], 0, q0, qtotal, outr, outi, xch, tws, rsrc, kbuf, lane, lane16, wave, gtw, w3);
+  br1f_row<true>(pk[0], 0, q0, qtotal, outr, outi, xch, tws, rsrc, kbuf, lane, lane16, wave, gtw, w3, tr);
 #pragma unroll 1
   for (int k = 1; k < D1; ++k)
-    br1f_row<false>(pk[0], k, q0 + k, qtotal, outr, outi, xch, tws, rsrc, kbuf, lane, lane16, wave, gtw, w3);
+    br1f_row<false>(pk[0], k, q0 + k, qtotal, outr, outi, xch, tws, rsrc, kbuf, lane, lane16, wave, gtw, w3, tr);
 #pragma unroll 1
   for (int k = 0; k < D1; ++k)
-    br1f_row<false>(pk[1], k, q0 + D1 + k, qtotal, outr, outi, xch, tws, rsrc, kbuf, lane, lane16, wave, gtw, w3);
-  F::inv_pair<true>(outr, outi, xch, tws, lane, gtw, w3);  // both outputs, interleaved
+    br1f_row<false>(pk[1], k, q0 + D1 + k, qtotal, outr, outi, xch, tws, rsrc, kbuf, lane, lane16, wave, gtw, w3,
+                    tr);
+  F::inv_pair<true, true>(outr, outi, xch, tws, lane, gtw, w3, tr);  // both outputs, interleaved
 #pragma unroll
   for (int o = 0; o < 2; ++o)
 #pragma unroll
@@ -324,6 +326,21 @@ __device__ __forceinline__ void br1f_body(
   // transform (LDS runs at ~60 % of its bandwidth here; 595 -> 591 ms per 16,384 messages,
   // profiles/r04/br1f_w3_ab.log)
   const double2 w3[2] = {tws[Fft512::TW_P3 + lane], tws[Fft512::TW_P3 + 64 + lane]};
+  // the forward's pass-0 (c, t) and pass-1 (c, t) in registers for the whole rotation (Tw1Reg)
+  Tw1Reg tr;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const double2 v = tws[Fft512::TW_P0F + k];
+    tr.f0c[k] = v.x;
+    const uint64_t y = __builtin_bit_cast(uint64_t, v.y);  // wave-uniform: readfirstlane keeps it in SGPRs
+    tr.f0t[k] = __builtin_bit_cast(double, (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)y) |
+                                               ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(y >> 32)) << 32));
+  }
+#pragma unroll
+  for (int e0 = 0; e0 < 2; ++e0) {
+    tr.p1[2 * e0] = tws[Fft512::tw4_index(lane, e0, 0)];
+    tr.p1[2 * e0 + 1] = tws[Fft512::tw4_index(lane, e0, 1)];
+  }
   // every step runs (a = 0 gives zero digits and leaves ACC unchanged) so the waves share the
   // staged key rows; row 0 is issued before the loop
   const __amdgpu_buffer_rsrc_t rsrc = bsk1_rsrc(bskf);
@@ -333,7 +350,7 @@ __device__ __forceinline__ void br1f_body(
 #pragma unroll 1
   for (int i = 0; i < N0; ++i) {
     const int a = __builtin_amdgcn_readfirstlane(la[i]);
-    br1f_step_lds<G>(ac, xch, tws, a, rsrc, i * 2 * D1, N0 * 2 * D1, kbuf, lane, lane16, wave, tb.fft1, w3, rg);
+    br1f_step_lds<G>(ac, xch, tws, a, rsrc, i * 2 * D1, N0 * 2 * D1, kbuf, lane, lane16, wave, tb.fft1, w3, rg, tr);
   }
   rg.publish(margin);
   __syncthreads();

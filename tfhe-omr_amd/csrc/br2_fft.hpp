@@ -215,10 +215,14 @@ struct Fft1024 {
     __device__ void operator()() const {}
   };
   // mid(): called after the cross-wave exchange (br2f_digit issues key loads there)
+  // p0: pass 0's R2, C8, T8 held in VGPRs by the caller (else SGPR constants)
   template <typename Mid = NoMid>
   __device__ static __forceinline__ void fwd(double (&xr)[E], double (&xi)[E], double2 *X, int t,
-                                             const double2 (&wc)[4][2], Mid mid = Mid()) {
-    fwd_pass_t(xr, xi, make_double2(R2, 1.0), make_double2(C8, T8));
+                                             const double2 (&wc)[4][2], Mid mid = Mid(), const double *p0 = nullptr) {
+    if (p0)
+      fwd_pass_t(xr, xi, make_double2(p0[0], 1.0), make_double2(p0[1], p0[2]));
+    else
+      fwd_pass_t(xr, xi, make_double2(R2, 1.0), make_double2(C8, T8));
     perm(xr, xi);
     fwd_pass_t(xr, xi, wc[0][0], wc[0][1]);
     exchange<1, 2, 0, true>(xr, xi, X, t);
@@ -358,7 +362,8 @@ template <int W>
 __device__ __forceinline__ void br2f_digit(const uint32_t (&pk)[2][Fft1024::E][Digits2S::DW], int j, int q, int nx,
                                            double (&sr)[2][2][Fft1024::E], double (&si)[2][2][Fft1024::E],
                                            double2 (&ka)[2][Fft1024::E], double2 (&kb)[2][Fft1024::E], double2 *X,
-                                           __amdgpu_buffer_rsrc_t rsrc, uint32_t t16, int t, const double2 (&wc)[4][2]) {
+                                           __amdgpu_buffer_rsrc_t rsrc, uint32_t t16, int t, const double2 (&wc)[4][2],
+                                           const double *p0) {
   using F = Fft1024;
   constexpr int E = F::E;
   double xr[E], xi[E];
@@ -390,7 +395,7 @@ __device__ __forceinline__ void br2f_digit(const uint32_t (&pk)[2][Fft1024::E][D
     __builtin_amdgcn_s_setprio(2);
 #pragma unroll
     for (int l = 0; l < LE; ++l) load_kb(l);
-  });
+  }, p0);
 #pragma unroll
   for (int l = LE; l < 2; ++l) load_kb(l);
 #pragma unroll
@@ -608,6 +613,15 @@ __device__ __forceinline__ void br2f_body(const uint32_t *__restrict__ lwe_int, 
   F::block_ct<2>(wc[1], twg, t);
   F::block_ct<3>(wc[2], twg, t);
   F::block_ct<4>(wc[3], twg, t);
+#ifndef OMR_BR2_P0V
+#define OMR_BR2_P0V 0
+#endif
+  double p0v[3] = {F::R2, F::C8, F::T8};
+  if constexpr (OMR_BR2_P0V) {  // in VGPRs (opaque copies), not SGPR constants
+#pragma unroll
+    for (int k = 0; k < 3; ++k) asm volatile("v_mov_b64 %0, %1" : "=v"(p0v[k]) : "s"(p0v[k]));
+  }
+  const double *p0 = OMR_BR2_P0V ? p0v : nullptr;
   double2 ka[2][E], kb[2][E];
   const __amdgpu_buffer_rsrc_t rsrc = bsk2_rsrc(bskf);
   const uint32_t t16 = (uint32_t)t * 16u;
@@ -645,8 +659,8 @@ __device__ __forceinline__ void br2f_body(const uint32_t *__restrict__ lwe_int, 
       }
 #pragma unroll 1
       for (int j = 0; j < D2 / 2; ++j) {
-        br2f_digit<0>(pk, j, q0 + p * D2 + j, nxt(j, 0), sr, si, ka, kb, Xb[0], rsrc, t16, t, wc);
-        br2f_digit<1>(pk, j, q0 + p * D2 + j + 3, nxt(j, 1), sr, si, ka, kb, Xb[1], rsrc, t16, t, wc);
+        br2f_digit<0>(pk, j, q0 + p * D2 + j, nxt(j, 0), sr, si, ka, kb, Xb[0], rsrc, t16, t, wc, p0);
+        br2f_digit<1>(pk, j, q0 + p * D2 + j + 3, nxt(j, 1), sr, si, ka, kb, Xb[1], rsrc, t16, t, wc, p0);
       }
     }
     // inverses on X0, X1, X0, X1, rounding to the exact limb products, recombination mod q2

@@ -102,6 +102,15 @@ __device__ __forceinline__ void ibfly(double &pr, double &pi, double &qr, double
 // of P0's A, B, C, w8 C; 11 + 2 blk + (A, B) (c, t) of P1's block blk = (j8 j7 j6); 27 + (t - 1) 32
 // + hi, hi = j8..j4 = lane & 31, P2's T_t (inverse); 251 + 32 k + hi the (c, t) of P2's A, B, C,
 // w8 C; 379 + 64 e1 + lane the (c, t) of P3's stage-8 twiddle of the even sibling.
+// Twiddles br1f keeps in registers for its whole loop (round 6): pass 1's (c, t) of A and B of the
+// lane's two blocks (p1: 16 VGPRs instead of 4 ds_read_b128 on the critical path of every transform)
+// and pass 0's forward (c, t): c per lane (VGPRs, as before), t wave-uniform (SGPRs: the 8 VGPRs that
+// make room for p1). Level 1 -1.6 to -2.2 % over six same-box runs (profiles/r06d, r06e).
+struct Tw1Reg {
+  double f0c[4], f0t[4];
+  double2 p1[4];
+};
+
 template <int T_, int E_, int L_>
 struct WgFft {
   static constexpr int T = T_, E = E_, L = L_, N = T * E;
@@ -198,12 +207,18 @@ struct WgFft {
     return tws[TW_P2F + k * 32 + (lane & 31)];
   }
 
-  template <int P, int C, bool G = false>
+  template <int P, int C, bool G = false, bool R = false>
   __device__ static __forceinline__ void fwd8(double (&xr)[C][E], double (&xi)[C][E], const double2 *tws,
-                                              int lane, const double2 *__restrict__ gtw = nullptr) {
+                                              int lane, const double2 *__restrict__ gtw = nullptr,
+                                              const Tw1Reg &tr = Tw1Reg{}) {
     double2 ct[4];  // (c, t) of A, B, C, w8 C, all requested before the first use (one LDS round trip)
 #pragma unroll
-    for (int k = 0; k < 4; ++k) ct[k] = ct8<P, G>(tws, gtw, k, lane);
+    for (int k = 0; k < 4; ++k) {
+      if constexpr (P == 0 && R)
+        ct[k] = make_double2(tr.f0c[k], tr.f0t[k]);
+      else
+        ct[k] = ct8<P, G>(tws, gtw, k, lane);
+    }
     if constexpr (P != 0) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int c = 0; c < C; ++c) {
@@ -280,11 +295,13 @@ struct WgFft {
   __device__ static __forceinline__ int tw4_index(int lane, int e0, int k) {  // k: 0 A, 1 B
     return TW_P1 + 2 * ((((lane >> 4) & 3) << 1) | e0) + k;
   }
-  template <int C>
-  __device__ static __forceinline__ void fwd4(double (&xr)[C][E], double (&xi)[C][E], const double2 *tws, int lane) {
+  template <int C, bool R = false>
+  __device__ static __forceinline__ void fwd4(double (&xr)[C][E], double (&xi)[C][E], const double2 *tws, int lane,
+                                              const Tw1Reg &tr = Tw1Reg{}) {
 #pragma unroll
     for (int e0 = 0; e0 < 2; ++e0) {
-      const double2 A = tws[tw4_index(lane, e0, 0)], B = tws[tw4_index(lane, e0, 1)];
+      const double2 A = R ? tr.p1[2 * e0] : tws[tw4_index(lane, e0, 0)];
+      const double2 B = R ? tr.p1[2 * e0 + 1] : tws[tw4_index(lane, e0, 1)];
       const int r0 = e0, r1 = e0 | 2, r2 = e0 | 4, r3 = e0 | 6;
 #pragma unroll
       for (int c = 0; c < C; ++c) {
@@ -296,11 +313,13 @@ struct WgFft {
       }
     }
   }
-  template <int C>
-  __device__ static __forceinline__ void inv4(double (&xr)[C][E], double (&xi)[C][E], const double2 *tws, int lane) {
+  template <int C, bool R = false>
+  __device__ static __forceinline__ void inv4(double (&xr)[C][E], double (&xi)[C][E], const double2 *tws, int lane,
+                                              const Tw1Reg &tr = Tw1Reg{}) {
 #pragma unroll
     for (int e0 = 0; e0 < 2; ++e0) {
-      const double2 A = tws[tw4_index(lane, e0, 0)], B = tws[tw4_index(lane, e0, 1)];
+      const double2 A = R ? tr.p1[2 * e0] : tws[tw4_index(lane, e0, 0)];
+      const double2 B = R ? tr.p1[2 * e0 + 1] : tws[tw4_index(lane, e0, 1)];
       const int r0 = e0, r1 = e0 | 2, r2 = e0 | 4, r3 = e0 | 6;
 #pragma unroll
       for (int c = 0; c < C; ++c) {
@@ -348,14 +367,14 @@ struct WgFft {
   // C transforms at once (lds holds C * BUF complex)
   // G: pass-0 twiddles from the global table gtw (must be non-null); w3: pass 3's two twiddles of
   // this lane held in registers by the caller (else read from tws)
-  template <int C, bool G = false>
+  template <int C, bool G = false, bool R = false>
   __device__ static __forceinline__ void fwd(double (&xr)[C][E], double (&xi)[C][E], double2 *lds,
                                              const double2 *tws, int lane,
                                              const double2 *__restrict__ gtw = nullptr,
-                                             const double2 *w3 = nullptr) {
-    fwd8<0, C, G>(xr, xi, tws, lane, gtw);
+                                             const double2 *w3 = nullptr, const Tw1Reg &tr = Tw1Reg{}) {
+    fwd8<0, C, G, R>(xr, xi, tws, lane, gtw, tr);
     swap01<C>(xr, xi);
-    fwd4<C>(xr, xi, tws, lane);
+    fwd4<C, R>(xr, xi, tws, lane, tr);
     exchange<C, 1, 2>(xr, xi, lds, lane);
     fwd8<2, C>(xr, xi, tws, lane);
     swap23<C>(xr, xi);
@@ -377,11 +396,11 @@ struct WgFft {
   // both (C = 2), the LDS exchange of the second follows the first's in the same slots (one
   // wave's LDS operations complete in order; the fence keeps the compiler from hoisting the
   // second's writes above the first's reads).
-  template <bool G = false>
+  template <bool G = false, bool R = false>
   __device__ static __forceinline__ void inv_pair(double (&xr)[2][E], double (&xi)[2][E], double2 *lds,
                                                   const double2 *tws, int lane,
                                                   const double2 *__restrict__ gtw = nullptr,
-                                                  const double2 *w3 = nullptr) {
+                                                  const double2 *w3 = nullptr, const Tw1Reg &tr = Tw1Reg{}) {
     inv2<2>(xr, xi, tws, lane, w3);
     swap23<2>(xr, xi);
     inv8<2, 2>(xr, xi, tws, lane);
@@ -389,7 +408,7 @@ struct WgFft {
     for (int c = 0; c < 2; ++c)
       exchange<1, 2, 1>(reinterpret_cast<double(&)[1][E]>(xr[c]), reinterpret_cast<double(&)[1][E]>(xi[c]), lds,
                         lane);
-    inv4<2>(xr, xi, tws, lane);
+    inv4<2, R>(xr, xi, tws, lane, tr);
     swap01<2>(xr, xi);
     inv8<0, 2, G>(xr, xi, tws, lane, gtw);
   }
