@@ -365,3 +365,35 @@ def test_apriori_bound_below_half_on_gpu_generated_keys(pack_seed, key_seed):
         assert det.exactness() == {"guarded": [False, False], "breaches": [0, 0]}
     finally:
         det.close()
+
+
+def test_apriori_bound_margin_over_16_gpu_keys():
+    """The exactness margin over 16 GPU-generated keys (E2 rose to 0.445 with the
+    tangent-form forward transforms, 0.055 below the threshold at which a context guards level 2 on
+    every launch). Reports every key's E1 / E2 and the maxima; every key must stay below 0.5 (else
+    its context would be guarded automatically: still exact, but on the guarded kernels)."""
+    import torch
+    dev = torch.device("cuda", 0)
+    rows = []
+    for i in range(16):
+        pack_seed, key_seed = 1000 + 37 * i, 11 + i
+        pack = A.SecretKeyPack(pack_seed)
+        bufs = [torch.empty(int(np.prod(shape)), dtype=dt, device=dev)
+                for shape, dt in ((A.BSK1_SHAPE, torch.int32), (A.KSK_SHAPE, torch.int32),
+                                  (A.BSK2_SHAPE, torch.int64), (A.TK_SHAPE, torch.int64))]
+        pack.generate_detection_key_device(key_seed, *[b.data_ptr() for b in bufs])
+        det = A.Detector.from_device_key(*[b.data_ptr() for b in bufs])
+        try:
+            rm = det.rounding_margin()
+            rows.append((pack_seed, key_seed, rm["apriori"][0], rm["apriori"][1], rm["kappa"][0], rm["kappa"][1],
+                         det.exactness()["guarded"]))
+        finally:
+            det.close()
+        del bufs
+    print("\npack  key   E1      E2      kappa1     kappa2     guarded")
+    for r in rows:
+        print(f"{r[0]:5d} {r[1]:4d}  {r[2]:.4f}  {r[3]:.4f}  {r[4]:.4e} {r[5]:.4e} {r[6]}")
+    e1, e2 = max(r[2] for r in rows), max(r[3] for r in rows)
+    print(f"max E1 {e1:.4f}, max E2 {e2:.4f} over {len(rows)} keys (margin to 0.5: {0.5 - e2:.4f})")
+    assert e1 < 0.5 and e2 < 0.5, (e1, e2)
+    assert all(r[6] == [False, False] for r in rows)

@@ -137,6 +137,19 @@ struct Fft1024 {
       cmulc(xr[3], xi[3], AB.x, AB.y);
     }
   }
+  // inv_pass with the pass's (B, A, AB) already loaded (w)
+  __device__ static __forceinline__ void inv_pass_w(double (&xr)[E], double (&xi)[E], const double2 (&w)[3]) {
+    inet4(xr, xi);
+    cmulc(xr[1], xi[1], w[0].x, w[0].y);
+    cmulc(xr[2], xi[2], w[1].x, w[1].y);
+    cmulc(xr[3], xi[3], w[2].x, w[2].y);
+  }
+  template <int P>
+  __device__ static __forceinline__ void inv_tw(double2 (&w)[3], const double2 *tws, int t) {
+    const int b = block<P>(t);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) w[k] = tws[tw_slot(P, b, k)];
+  }
   // P0 <-> P1 and P2 <-> P3 (an involution): register bit 1 <-> lane bit 5, register bit 0 <-> lane bit 4
   __device__ static __forceinline__ void perm(double (&xr)[E], double (&xi)[E]) {
     swap_lane_bit<5>(xr[0], xr[2]);
@@ -215,14 +228,10 @@ struct Fft1024 {
     __device__ void operator()() const {}
   };
   // mid(): called after the cross-wave exchange (br2f_digit issues key loads there)
-  // p0: pass 0's R2, C8, T8 held in VGPRs by the caller (else SGPR constants)
   template <typename Mid = NoMid>
   __device__ static __forceinline__ void fwd(double (&xr)[E], double (&xi)[E], double2 *X, int t,
-                                             const double2 (&wc)[4][2], Mid mid = Mid(), const double *p0 = nullptr) {
-    if (p0)
-      fwd_pass_t(xr, xi, make_double2(p0[0], 1.0), make_double2(p0[1], p0[2]));
-    else
-      fwd_pass_t(xr, xi, make_double2(R2, 1.0), make_double2(C8, T8));
+                                             const double2 (&wc)[4][2], Mid mid = Mid()) {
+    fwd_pass_t(xr, xi, make_double2(R2, 1.0), make_double2(C8, T8));
     perm(xr, xi);
     fwd_pass_t(xr, xi, wc[0][0], wc[0][1]);
     exchange<1, 2, 0, true>(xr, xi, X, t);
@@ -237,15 +246,22 @@ struct Fft1024 {
   // exchange first, in the wave's own quarter of X (which the previous use of X, two cross-wave
   // uses back, has finished with behind the last barrier), then the cross-wave one (own-quarter
   // writes)
+  // Each pass's (B, A, AB) is requested one pass ahead, before the previous pass's arithmetic (round 6:
+  // level 2 -0.4 %, profiles/r06f/ab.log), so its LDS round trip is off the pass's critical path.
   __device__ static __forceinline__ void inv(double (&xr)[E], double (&xi)[E], double2 *X, const double2 *tws, int t) {
-    inv_pass<4>(xr, xi, tws, t);
+    double2 w4[3], w3[3], w2[3], w1[3];
+    inv_tw<4>(w4, tws, t);
+    inv_tw<3>(w3, tws, t);
+    inv_pass_w(xr, xi, w4);
     exchange<4, 3, 3, false>(xr, xi, X, t);
-    inv_pass<3>(xr, xi, tws, t);
+    inv_tw<2>(w2, tws, t);
+    inv_pass_w(xr, xi, w3);
     perm(xr, xi);
-    inv_pass<2>(xr, xi, tws, t);
+    inv_tw<1>(w1, tws, t);
+    inv_pass_w(xr, xi, w2);
     exchange<2, 1, 1, true>(xr, xi, X, t);
     __builtin_amdgcn_s_setprio(2);  // raised past the cross-wave barrier, as in br2f_digit
-    inv_pass<1>(xr, xi, tws, t);
+    inv_pass_w(xr, xi, w1);
     perm(xr, xi);
     inv_pass<0>(xr, xi, tws, t);
     __builtin_amdgcn_s_setprio(0);
@@ -362,8 +378,7 @@ template <int W>
 __device__ __forceinline__ void br2f_digit(const uint32_t (&pk)[2][Fft1024::E][Digits2S::DW], int j, int q, int nx,
                                            double (&sr)[2][2][Fft1024::E], double (&si)[2][2][Fft1024::E],
                                            double2 (&ka)[2][Fft1024::E], double2 (&kb)[2][Fft1024::E], double2 *X,
-                                           __amdgpu_buffer_rsrc_t rsrc, uint32_t t16, int t, const double2 (&wc)[4][2],
-                                           const double *p0) {
+                                           __amdgpu_buffer_rsrc_t rsrc, uint32_t t16, int t, const double2 (&wc)[4][2]) {
   using F = Fft1024;
   constexpr int E = F::E;
   double xr[E], xi[E];
@@ -395,7 +410,7 @@ __device__ __forceinline__ void br2f_digit(const uint32_t (&pk)[2][Fft1024::E][D
     __builtin_amdgcn_s_setprio(2);
 #pragma unroll
     for (int l = 0; l < LE; ++l) load_kb(l);
-  }, p0);
+  });
 #pragma unroll
   for (int l = LE; l < 2; ++l) load_kb(l);
 #pragma unroll
@@ -613,15 +628,6 @@ __device__ __forceinline__ void br2f_body(const uint32_t *__restrict__ lwe_int, 
   F::block_ct<2>(wc[1], twg, t);
   F::block_ct<3>(wc[2], twg, t);
   F::block_ct<4>(wc[3], twg, t);
-#ifndef OMR_BR2_P0V
-#define OMR_BR2_P0V 0
-#endif
-  double p0v[3] = {F::R2, F::C8, F::T8};
-  if constexpr (OMR_BR2_P0V) {  // in VGPRs (opaque copies), not SGPR constants
-#pragma unroll
-    for (int k = 0; k < 3; ++k) asm volatile("v_mov_b64 %0, %1" : "=v"(p0v[k]) : "s"(p0v[k]));
-  }
-  const double *p0 = OMR_BR2_P0V ? p0v : nullptr;
   double2 ka[2][E], kb[2][E];
   const __amdgpu_buffer_rsrc_t rsrc = bsk2_rsrc(bskf);
   const uint32_t t16 = (uint32_t)t * 16u;
@@ -659,8 +665,8 @@ __device__ __forceinline__ void br2f_body(const uint32_t *__restrict__ lwe_int, 
       }
 #pragma unroll 1
       for (int j = 0; j < D2 / 2; ++j) {
-        br2f_digit<0>(pk, j, q0 + p * D2 + j, nxt(j, 0), sr, si, ka, kb, Xb[0], rsrc, t16, t, wc, p0);
-        br2f_digit<1>(pk, j, q0 + p * D2 + j + 3, nxt(j, 1), sr, si, ka, kb, Xb[1], rsrc, t16, t, wc, p0);
+        br2f_digit<0>(pk, j, q0 + p * D2 + j, nxt(j, 0), sr, si, ka, kb, Xb[0], rsrc, t16, t, wc);
+        br2f_digit<1>(pk, j, q0 + p * D2 + j + 3, nxt(j, 1), sr, si, ka, kb, Xb[1], rsrc, t16, t, wc);
       }
     }
     // inverses on X0, X1, X0, X1, rounding to the exact limb products, recombination mod q2

@@ -1,15 +1,16 @@
-// Issue cost of an FP64 FMA whose multiplier is an SGPR pair vs a VGPR pair (round 6: the level-1
-// twiddle experiments). Each lane runs 8 independent FMA chains (enough ILP to keep
-// the FP64 pipe busy); the multiplier is either wave-uniform in SGPRs ("s" constraint) or held in a
-// VGPR pair ("v" constraint). 256 x 4 x W waves (W waves per SIMD).
+// Issue cost of an FP64 FMA whose multiplier is an SGPR pair vs a VGPR pair, and the FP64 rate one,
+// two and four waves per SIMD reach with CH independent FMA chains per lane (round 6: the level-1
+// twiddle experiments). The multiplier is either wave-uniform in SGPRs ("s"
+// constraint) or held in a VGPR pair ("v" constraint); UNR rounds of the CH chains per loop
+// iteration keep the branch out of the measurement. 256 x 4 x W waves (W waves per SIMD).
 //   hipcc -O3 --offload-arch=gfx950 tools/microbench_sgpr.hip -o tools/microbench_sgpr
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
 
-constexpr int ITER = 4096, CH = 8;
+constexpr int ITER = 512, UNR = 16;
 
-template <bool SGPR>
+template <bool SGPR, int CH>
 __global__ void k_fma(double *out, double w0) {
   double v[CH];
   for (int c = 0; c < CH; ++c) v[c] = threadIdx.x + c;
@@ -19,11 +20,11 @@ __global__ void k_fma(double *out, double w0) {
 #pragma unroll 1
   for (int i = 0; i < ITER; ++i) {
 #pragma unroll
-    for (int c = 0; c < CH; ++c) {
+    for (int c = 0; c < CH * UNR; ++c) {
       if constexpr (SGPR)
-        asm volatile("v_fma_f64 %0, %0, %1, 0.5" : "+v"(v[c]) : "s"(w));
+        asm volatile("v_fma_f64 %0, %0, %1, 0.5" : "+v"(v[c % CH]) : "s"(w));
       else
-        asm volatile("v_fma_f64 %0, %0, %1, 0.5" : "+v"(v[c]) : "v"(wv));
+        asm volatile("v_fma_f64 %0, %0, %1, 0.5" : "+v"(v[c % CH]) : "v"(wv));
     }
   }
   double r = 0;
@@ -33,32 +34,33 @@ __global__ void k_fma(double *out, double w0) {
 
 int main() {
   int cus = 0;
-  hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
   double *buf;
-  hipMalloc(&buf, (size_t)cus * 4 * 1024 * sizeof(double));
+  (void)hipMalloc(&buf, (size_t)cus * 4 * 1024 * sizeof(double));
   hipEvent_t a, b;
-  hipEventCreate(&a);
-  hipEventCreate(&b);
-  for (int wps = 1; wps <= 4; wps *= 2) {  // waves per SIMD: blocks of 256 threads, wps per CU
-    for (int s = 0; s < 2; ++s) {
-      float best = 1e30f;
-      for (int rep = 0; rep < 3; ++rep) {
-        hipEventRecord(a);
-        if (s)
-          k_fma<true><<<cus * wps, 256>>>(buf, 1.0000001);
-        else
-          k_fma<false><<<cus * wps, 256>>>(buf, 1.0000001);
-        hipEventRecord(b);
-        hipEventSynchronize(b);
-        float ms;
-        hipEventElapsedTime(&ms, a, b);
-        best = ms < best ? ms : best;
-      }
-      const double fmas = (double)cus * wps * 256 * ITER * CH;
-      printf("waves/SIMD %d  multiplier in %s: %.3f ms  %.1f G lane-FMA/s  (%.2f cycles per wave-FMA per SIMD at 2.4 GHz)\n",
-             wps, s ? "SGPR" : "VGPR", best, fmas / (best * 1e6), (best * 1e-3 * 2.4e9) / (fmas / 64 / (cus * 4)));
+  (void)hipEventCreate(&a);
+  (void)hipEventCreate(&b);
+  auto run = [&](auto kern, int wps, const char *what, int ch) {
+    float best = 1e30f;
+    for (int rep = 0; rep < 3; ++rep) {
+      (void)hipEventRecord(a);
+      kern<<<cus * wps, 256>>>(buf, 1.0000001);
+      (void)hipEventRecord(b);
+      (void)hipEventSynchronize(b);
+      float ms;
+      (void)hipEventElapsedTime(&ms, a, b);
+      best = ms < best ? ms : best;
     }
+    const double fmas = (double)cus * wps * 256 * ITER * UNR * ch;
+    printf("waves/SIMD %d  chains %2d  multiplier in %s: %.3f ms  %.1f G lane-FMA/s  (%.2f cycles per wave-FMA per SIMD at 2.4 GHz; 4 = FP64 peak)\n",
+           wps, ch, what, best, fmas / (best * 1e6), (best * 1e-3 * 2.4e9) / (fmas / 64 / (cus * 4)));
+  };
+  for (int wps = 1; wps <= 4; wps *= 2) {
+    run(k_fma<false, 8>, wps, "VGPR", 8);
+    run(k_fma<true, 8>, wps, "SGPR", 8);
+    run(k_fma<false, 16>, wps, "VGPR", 16);
+    run(k_fma<true, 16>, wps, "SGPR", 16);
   }
-  hipFree(buf);
+  (void)hipFree(buf);
   return 0;
 }
