@@ -206,26 +206,13 @@ __device__ __forceinline__ void br1f_row(const uint32_t (&pk)[16], int k, int q,
                                          const Tw1Reg &tr) {
   using F = Fft512;
   const bool more = q + 1 < qtotal;
-#ifndef OMR_BR1_DPRE
-#define OMR_BR1_DPRE 0
-#endif
-  double xr[1][8], xi[1][8];
-  if constexpr (OMR_BR1_DPRE) {  // the digits (registers only) before the barrier
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      xr[0][e] = Lvl1Off::digit_u(pk[e], k);
-      xi[0][e] = Lvl1Off::digit_u(pk[8 + e], k);
-      asm volatile("" : "+v"(xr[0][e]), "+v"(xi[0][e]));  // materialised here, not sunk past the barrier
-    }
-  }
   wg_barrier_lds();  // every wave has finished reading buffer (q + 1) & 1 (row q - 1)
   if (more) krow_issue(rsrc, q + 1, kbuf + ((q + 1) & 1) * KROW_SLOTS, lane16, wave);
-  if constexpr (!OMR_BR1_DPRE) {
+  double xr[1][8], xi[1][8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      xr[0][e] = Lvl1Off::digit_u(pk[e], k);
-      xi[0][e] = Lvl1Off::digit_u(pk[8 + e], k);
-    }
+  for (int e = 0; e < 8; ++e) {
+    xr[0][e] = Lvl1Off::digit_u(pk[e], k);
+    xi[0][e] = Lvl1Off::digit_u(pk[8 + e], k);
   }
   F::fwd<1, true, true>(xr, xi, xch, tws, lane, gtw, w3, tr);
   if (more)
@@ -358,9 +345,6 @@ __device__ __forceinline__ void br1f_body(
   // staged key rows; row 0 is issued before the loop
   const __amdgpu_buffer_rsrc_t rsrc = bsk1_rsrc(bskf);
   const uint32_t lane16 = (uint32_t)lane * 16u;
-#ifdef OMR_BR1_PRIO
-  if (item & 1) __builtin_amdgcn_s_setprio(1);  // static priority for every other workgroup
-#endif
   krow_issue(rsrc, 0, kbuf, lane16, wave);
   RoundGuard<G> rg;
 #pragma unroll 1
