@@ -204,45 +204,6 @@ def test_latency_level2_fft_two_cu_matches_ntt(real, monkeypatch):
         slow.close()
 
 
-def test_latency_level2_fft_four_cu_matches_ntt(real, monkeypatch):
-    """The latency path's level 2 over four CUs per message (br2z_kernel: a context created with
-    OMR_BR2Z=1; it runs when the a priori bound of its accumulation order is below 0.5) against the
-    exact modular-NTT two-CU kernel (br2x_kernel, OMR_BR2Y=0) on the same level-1 outputs, bit for
-    bit, rotation and rotation + trace, at 1, 7, 20 and 64 messages (4, 28, 80 and 256 CUs; the
-    first two with two key-prefetch helpers per worker), and at 7 without helpers (OMR_PREFETCH=0)
-    and with the sc1 hand-off kept between workers on one XCD (OMR_FAST_HANDOFF=0)."""
-    _, _, dk = PL.keys()
-    monkeypatch.setenv("OMR_BR2Y", "0")
-    ntt = A.Detector(dk)
-    monkeypatch.delenv("OMR_BR2Y")
-    monkeypatch.setenv("OMR_BR2Z", "1")
-    z = A.Detector(dk)
-    monkeypatch.setenv("OMR_PREFETCH", "0")
-    nopf = A.Detector(dk)
-    monkeypatch.delenv("OMR_PREFETCH")
-    monkeypatch.setenv("OMR_FAST_HANDOFF", "0")
-    slow = A.Detector(dk)
-    monkeypatch.delenv("OMR_FAST_HANDOFF")
-    monkeypatch.delenv("OMR_BR2Z")
-    try:
-        for n in (1, 7, 20, 64):
-            mask = np.zeros(n, dtype=bool)
-            mask[::5] = True
-            ca, cb = PL.mixed_clues(mask, seed=1300 + n)
-            fl = ntt.first_level(ca, cb)
-            want = ntt.blind_rotate_level2(fl)
-            assert np.array_equal(z.blind_rotate_level2(fl), want), n
-            assert np.array_equal(z.second_level(fl), ntt.second_level(fl)), n
-            if n == 7:
-                assert np.array_equal(nopf.blind_rotate_level2(fl), want)
-                assert np.array_equal(slow.blind_rotate_level2(fl), want)
-    finally:
-        ntt.close()
-        z.close()
-        nopf.close()
-        slow.close()
-
-
 def test_level2_throughput_small_batches(real):
     """The throughput level-2 kernel (br2f_kernel, FFT) at batches of 5 and 6 messages against the
     latency kernels (the oracle-checked NTT path), rotation and rotation + trace."""

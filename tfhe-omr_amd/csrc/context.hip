@@ -18,7 +18,6 @@
 
 #include "br1_ntt.hpp"
 #include "br2_fft.hpp"
-#include "br2z.hpp"
 #include "detect_kernels.hpp"
 #include "encode_kernels.hpp"
 #include "key_spectra.hpp"
@@ -244,13 +243,11 @@ std::vector<CDD> dd_tree_twiddles(int L) {
 // 256-thread group chains its three rows (its j-th at weight 2 (3 - j)), then two additions (the
 // two groups' partials, the partner workgroup's) add 1 each: weight 8 - 2 j for digit 3 g + j.
 // Level 4: the fused FFT trace (br2f_trace): 11 steps, 25 rows (digits |d| <= 3) accumulated in
-// order, the trace key's rows [11 * 25][2 out][2 limb] as kmax. Level 5: level 2 as br2z_kernel
-// accumulates it: each worker chains its three rows (the j-th at weight 2 (3 - j)), then three
-// additions of the other workers' partials: weight 9 - 2 j for digit 3 h + j.
+// order, the trace key's rows [11 * 25][2 out][2 limb] as kmax.
 double apriori_bound(int level, const std::vector<double> &kmax) {
   const double u = 0x1p-53;
-  const bool y = level == 3, tr = level == 4, z = level == 5;
-  if (y || tr || z) level = 2;
+  const bool y = level == 3, tr = level == 4;
+  if (y || tr) level = 2;
   const int n = level == 1 ? 512 : 1024, R = level == 1 ? 2 * D1 : tr ? DT : 2 * D2, O = level == 1 ? 2 : 4;
   const int steps = level == 1 ? N0 : tr ? TRACE_STEPS : NI;
   // accumulation order of the kernels' MAC: br1f / br1l rows 0..7; br2f digits in issue order
@@ -268,10 +265,7 @@ double apriori_bound(int level, const std::vector<double> &kmax) {
         const int r = level == 1 || tr ? k : order2[k];
         const double kap = kmax[((size_t)i * R + r) * O + o];
         s += kap;
-        w += (y   ? 8.0 - 2.0 * ((r % D2) % 3)
-              : z ? 9.0 - 2.0 * ((r % D2) % 3)
-                  : 2.0 * R - 2.0 * k) *
-             kap;
+        w += (y ? 8.0 - 2.0 * ((r % D2) % 3) : 2.0 * R - 2.0 * k) * kap;
       }
       worst = std::max(worst, cf * s + cw * w);
     }
@@ -342,10 +336,6 @@ struct omr_ctx {
   // not guarded; br2x_kernel's NTT otherwise
   double apriori_y = 1.0;
   bool br2y = true;
-  // OMR_BR2Z=1 at context creation: the latency path's level 2 over four CUs per message
-  // (br2z_kernel) instead of br2y, when its bound (apriori_bound level 5) proves it exact
-  double apriori_z = 1.0;
-  bool br2z = false;
   bool no_prefetch = false;  // OMR_PREFETCH=0: the latency kernels launch no key-prefetch helpers
   bool no_fast_handoff = false;  // OMR_FAST_HANDOFF=0: br2y keeps the sc1 hand-off on one XCD too
   // host-API staging
@@ -645,12 +635,11 @@ omr_status launch_br2x(omr_ctx *c, size_t n, const uint32_t *lwe_int, uint64_t *
     dev_free(c->x_slots);
     dev_free(c->x_flags);
     c->x_cap = 0;
-    // br2y: [n][2][2 slot][2 limb][2][1024]; br2z: [n][4][2 slot][4][2][1024]
-    HIP_TRY(hipMalloc(&c->x_slots, n * 32 * N2 * sizeof(double)));
-    HIP_TRY(hipMalloc(&c->x_flags, n * 8 * sizeof(uint32_t)));  // br2y / br2z: + the workers' XCD ids
+    HIP_TRY(hipMalloc(&c->x_slots, n * 8 * N2 * sizeof(double)));  // br2y: [n][2][2 slot][2 limb][2][1024]
+    HIP_TRY(hipMalloc(&c->x_flags, n * 4 * sizeof(uint32_t)));  // br2y: + the workers' XCD ids
     c->x_cap = n;
   }
-  HIP_TRY(hipMemsetAsync(c->x_flags, 0, n * 8 * sizeof(uint32_t), st));
+  HIP_TRY(hipMemsetAsync(c->x_flags, 0, n * 4 * sizeof(uint32_t), st));
   const double *bsk2 = c->bsk2;
   DeviceTables tb = c->tb;
   double *slots = c->x_slots;
@@ -661,27 +650,6 @@ omr_status launch_br2x(omr_ctx *c, size_t n, const uint32_t *lwe_int, uint64_t *
   // br2y_kernel (FFT) when the bound of its accumulation order proves it exact and level 2 is not
   // guarded; br2x_kernel's exact NTT otherwise (same arguments apart from the key form)
   const bool y = c->br2y && !guarded(c, 1) && c->apriori_y < 0.5;
-  // br2z: four workers per message in rows 0..3, plus 4 BR2Z_H rows of key prefetchers when every
-  // workgroup still gets a CU of its own; br2y when the four workers do not fit
-  if (c->br2z && !guarded(c, 1) && c->apriori_z < 0.5) {
-    const int nmsg = (int)n, w8 = (nmsg + 7) / 8 * 8, allow_fast = c->no_fast_handoff ? 0 : 1;
-    const int rows = (size_t)w8 * (4 + 4 * BR2Z_H) <= (size_t)c->num_cu && !c->no_prefetch ? 4 + 4 * BR2Z_H : 4;
-    if ((size_t)w8 * rows <= (size_t)c->num_cu) {
-      const double2 *bskf = c->bsk2f, *twg = c->fft2;
-      void *args_z[] = {(void *)&lwe_int, (void *)&bskf, (void *)&twg, (void *)&tb, (void *)&slots, (void *)&flags,
-                        (void *)&err, (void *)&out, (void *)&nmsg, (void *)&w8, (void *)&allow_fast};
-      const hipError_t e = hipLaunchCooperativeKernel(reinterpret_cast<const void *>(&br2z_kernel),
-                                                      dim3((unsigned)(w8 * rows)), dim3(BR2Z_T), args_z, 0, st);
-      if (e == hipSuccess) {
-        HIP_TRY(hipMemcpyAsync(c->x_err_host, c->x_err, sizeof(int), hipMemcpyDeviceToHost, st));
-        *launched = true;
-        return OMR_OK;
-      }
-      if (e != hipErrorCooperativeLaunchTooLarge && e != hipErrorNotSupported && e != hipErrorInvalidConfiguration)
-        return set_error(OMR_ERR_DEVICE, std::string("br2z cooperative launch: ") + hipGetErrorString(e));
-      (void)hipGetLastError();  // refused: nothing was enqueued; br2y below
-    }
-  }
   const double2 *bskf = c->bsk2f, *twg = c->fft2;
   // br2y: message m in column m of a grid w8 = n rounded up to 8 columns wide, its mask / body
   // workers in rows 0 / 1, plus 2 BR2Y_H rows of key prefetchers (br2_fft.hpp) when every workgroup
@@ -831,8 +799,6 @@ extern "C" omr_status omr_ctx_create(const omr_detection_key_view *key, int devi
     c->coop = coop != 0 && !(env && env[0] == '0');
     const char *ey = getenv("OMR_BR2Y");
     c->br2y = !(ey && ey[0] == '0');
-    const char *ez = getenv("OMR_BR2Z");
-    c->br2z = ez && ez[0] == '1';
     const char *ep = getenv("OMR_PREFETCH");
     c->no_prefetch = ep && ep[0] == '0';
     const char *eh = getenv("OMR_FAST_HANDOFF");
@@ -953,7 +919,6 @@ extern "C" omr_status omr_ctx_create(const omr_detection_key_view *key, int devi
     c->apriori[0] = apriori_bound(1, k1);
     c->apriori[1] = apriori_bound(2, k2);
     c->apriori_y = apriori_bound(3, k2);
-    c->apriori_z = apriori_bound(5, k2);
     c->apriori_t = apriori_bound(4, kt);
     c->trace_fft = c->apriori_t < 0.5;
     // the exactness contract: a level whose bound does not prove every rounding exact is guarded

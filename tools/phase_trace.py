@@ -35,12 +35,9 @@ names = {  # phase ending at mark k (k = 1..7); br2x has no mark 2 (a mark there
     "br2y": {1: "barrier + digits", 2: "3 fwd + MAC", 3: "limb-swap writes + barrier",
              4: "sums + sc1 stores + vmcnt + barrier", 5: "flag + poll + barrier", 6: "sc1 loads + inverse",
              7: "round + half swap + barrier + update"},
-    "br2z": {1: "barrier + digits", 2: "3 fwd (interleaved)", 3: "kb wait + MAC", 4: "stores + vmcnt + barrier",
-             5: "flag + poll 3 + barrier", 6: "sc1 loads + sums", 7: "2 inv (interleaved) + update"},
 }
 for slot in range(24):
-    kern = "br1l" if slot < 8 else ("br2x" if os.environ.get("OMR_BR2Y") == "0" else
-                                    "br2z" if os.environ.get("OMR_BR2Z") == "1" else "br2y")
+    kern = "br1l" if slot < 8 else ("br2x" if os.environ.get("OMR_BR2Y") == "0" else "br2y")
     m = marks[slot]
     if not m[:, 0].any():
         continue
@@ -50,7 +47,6 @@ for slot in range(24):
     present = [k for k in range(PT_K) if m[:, k].all()]  # marks this wave records
     parts = "  ".join(f"{names[kern].get(k1, f'->{k1}')} {(m[:, k1] - m[:, k0]).mean():.0f}"
                       for k0, k1 in zip(present, present[1:]))
-    per = 4 if kern == "br2z" else 8  # waves per traced workgroup
-    lab = f"{kern} wg{(slot - 8) // per if slot >= 8 else 0} wave{(slot - 8) % per if slot >= 8 else slot}"
+    lab = f"{kern} wg{(slot - 8) // 8 if slot >= 8 else 0} wave{slot % 8}"
     print(f"{lab}: clock {mhz:.0f} MHz, step {step:.0f} cyc ({step / mhz:.2f} us) | {parts}", flush=True)
 det.close()
