@@ -339,8 +339,13 @@ __device__ __forceinline__ void br2f_load_half(double2 (&k)[2][Fft1024::E], __am
   for (int l = 0; l < 2; ++l)
 #pragma unroll
     for (int e = 0; e < Fft1024::E; ++e) {
+#ifdef OMR_BR2_KEYABL  // timing-only ablation: every key load from one 4 KB block (L1-resident; wrong output)
+      const uint32_t soff = 0;
+      (void)q;
+#else
       const uint32_t soff = (uint32_t)q * (uint32_t)(BR2_ROW * sizeof(double2)) +
                             (uint32_t)(((o * 2 + l) * Fft1024::n + e * Fft1024::T) * sizeof(double2));
+#endif
       k[l][e] = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rsrc, t16, (int)soff, 0));
     }
 }
@@ -393,8 +398,12 @@ __device__ __forceinline__ void br2f_digit(const uint32_t (&pk)[2][Fft1024::E][D
   auto load_kb = [&](int l) {
 #pragma unroll
     for (int e = 0; e < E; ++e) {
+#ifdef OMR_BR2_KEYABL
+      const uint32_t soff = 0;
+#else
       const uint32_t soff = (uint32_t)q * (uint32_t)(BR2_ROW * sizeof(double2)) +
                             (uint32_t)(((1 * 2 + l) * Fft1024::n + e * Fft1024::T) * sizeof(double2));
+#endif
       kb[l][e] = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rsrc, t16, (int)soff, 0));
     }
   };
